@@ -1,0 +1,205 @@
+"""Benchmark: cell updates per second (GCUPS) of the hot path on MI355X, plus roofline and CPU baseline.
+
+Workload (BASELINE.json metric "GCUPS at 65536^2 on 1 and 8 x MI355X"): a 65536 x 65536 torus, splitmix
+random 50 % fill generated on the device (data: synthetic).  One *step* = one pass of the streaming
+kernel that advances the whole board by `tblock` generations (temporal blocking).  For N GPUs (one
+process per GPU under torchrun) the board is 65536 wide and 65536*N tall, split into N row strips of
+65536^2 cells with RCCL halo exchange (weak scaling: per-GPU work fixed).
+
+    python bench.py                          # N = 1, defaults finish in well under a minute
+    python bench.py --steps 64 --warmup 4 --tblock 16
+    torchrun --nproc-per-node 8 bench.py --gpus 8
+
+Prints ONE JSON line (rank 0).  Inputs are resident in HBM before the timed region; the timed region is
+bracketed by barrier + device synchronize on both sides, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz (int32 lane-ops)
+OPS_PER_WORD_GEN = 13  # gol_bitlogic.h: 2 DPP + 2 alignbit + 9 bitop3 per 32 cells per generation
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--width", type=int, default=65536)
+    p.add_argument("--height", type=int, default=65536, help="rows per GPU (board height = height * gpus)")
+    p.add_argument("--tblock", type=int, default=16, help="generations per pass (1,2,4,8,16,24,32)")
+    p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU actor baseline sample length")
+    p.add_argument("--cpu-board", type=int, default=512, help="CPU actor baseline board side")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The C++ actor-protocol restatement (oracle/actor_protocol.cpp: GameOfLifeLogic.fs:39-71 message for
+    message) on this host's cores, bounded sample (~args.cpu_seconds of wall time)."""
+    exe = os.path.join(ROOT, "oracle", "build", "actor_protocol")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = args.cpu_board
+    out = subprocess.run([exe, str(n), str(n), "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"],
+                         check=True, capture_output=True, text=True, timeout=600).stdout
+    r = json.loads(out)
+    cpu = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": r["cell_updates_per_s"] / 1e9,
+        "unit": "GCUPS",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"actor-protocol restatement, {n}x{n} torus, dotnet-mod2 seed 42, {r['generations']} generations "
+        f"in {r['seconds']:.1f} s, {r['messages']} messages, {threads} threads on {cpu}",
+    }
+
+
+def load_traffic(path, key):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gameoflifewithactors_amd import TORUS, BOUNDED
+    from gameoflifewithactors_amd.strips import StripRunner
+
+    boundary = TORUS if args.boundary == "torus" else BOUNDED
+    W, H = args.width, args.height * world
+    k = args.tblock
+    runner = StripRunner(W, H, boundary, k, rank=rank, world=world, device=torch.device("cuda", local))
+    runner.seed_splitmix(args.seed)
+
+    for _ in range(args.warmup):
+        runner.step_pass()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    stream = runner.compute_stream
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        runner.step_pass()
+    ev1.record(stream)
+    barrier()
+    dt = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3  # HIP events on the stream the step kernels run on
+    if world > 1:
+        t = torch.tensor([dt, kernel_s], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, kernel_s = float(t[0]), float(t[1])
+
+    cells = W * H
+    gens = args.steps * k
+    gcups = cells * gens / dt / 1e9
+    # roofline of the dominant kernel, per launch (one launch = one pass of k generations per GPU)
+    cells_gpu = W * args.height
+    avg_launch_s = runner.kernel_time_per_pass(kernel_s, args.steps)
+    alg_bytes = 2 * cells_gpu / 8  # read + write the packed strip once per pass
+    achieved_gbs = alg_bytes / avg_launch_s / 1e9
+    valu_tops = OPS_PER_WORD_GEN * (cells_gpu / 32) * k / avg_launch_s / 1e12
+    traffic = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}")
+
+    result = None
+    if rank == 0:
+        result = {
+            "metric": "cell updates/sec (GCUPS) at 65536^2 per GPU",
+            "value": round(gcups, 3),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (bit-packed cells)",
+            "data": "synthetic (splitmix 50% fill generated on device)",
+            "config": {
+                "workload": f"{W}x{H} {args.boundary} board, {k} generations per step (temporal block), "
+                f"{world} row strip(s)",
+                "width": W,
+                "height": H,
+                "generations_per_step": k,
+                "boundary": args.boundary,
+                "seed": args.seed,
+                "parallelism": f"row strips x{world}" + (" (RCCL halo exchange)" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": f"gol_stream_step<K={k}>",
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_us": round(avg_launch_s * 1e6, 2),
+            },
+            "roofline_valu": {
+                "bound": "valu",
+                "achieved": round(valu_tops, 3),
+                "peak": round(VALU_PEAK_TOPS, 2),
+                "unit": "Tops/s (int32 lane-ops)",
+                "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
+                "ops_per_word_gen": OPS_PER_WORD_GEN,
+            },
+            "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
+        }
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

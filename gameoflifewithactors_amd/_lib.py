@@ -1,0 +1,121 @@
+"""ctypes binding of libgol_hip.so (the C ABI declared in include/gol/gol.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be loaded this module
+raises, and every Board operation goes through the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgol_hip.so")
+
+GOL_OK = 0
+GOL_ERR_INVALID = -1
+GOL_ERR_HIP = -2
+GOL_ERR_OOM = -3
+GOL_ERR_UNSUPPORTED = -4
+GOL_ERR_NO_DEVICE = -5
+
+TORUS = 0
+BOUNDED = 1
+INIT_DOTNET_MOD2 = 0
+INIT_DOTNET_NEXT2 = 1
+
+_ERRORS = {
+    GOL_ERR_INVALID: ValueError,
+    GOL_ERR_HIP: RuntimeError,
+    GOL_ERR_OOM: MemoryError,
+    GOL_ERR_UNSUPPORTED: NotImplementedError,
+    GOL_ERR_NO_DEVICE: RuntimeError,
+}
+
+
+class GolError(RuntimeError):
+    pass
+
+
+class Strip(ctypes.Structure):
+    """``gol_strip`` (include/gol/gol.h): geometry of one row strip of a (multi-GPU) board."""
+
+    _fields_ = [
+        ("width", ctypes.c_int64),
+        ("height", ctypes.c_int64),
+        ("y0", ctypes.c_int64),
+        ("rows", ctypes.c_int64),
+        ("ghost", ctypes.c_int64),
+        ("pitch", ctypes.c_int64),
+        ("boundary", ctypes.c_int32),
+        ("wrap_rows", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+i64 = ctypes.c_int64
+u64 = ctypes.c_uint64
+vp = ctypes.c_void_p
+u8p = ctypes.POINTER(ctypes.c_uint8)
+i64p = ctypes.POINTER(ctypes.c_int64)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+ip = ctypes.POINTER(ctypes.c_int)
+sp = ctypes.POINTER(Strip)
+
+# name -> (restype, argtypes).  Must cover every function include/gol/gol.h declares.
+SIGNATURES = {
+    "gol_create": (ctypes.c_int, [i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+    "gol_destroy": (ctypes.c_int, [vp]),
+    "gol_set_cells": (ctypes.c_int, [vp, u8p, i64]),
+    "gol_get_cells": (ctypes.c_int, [vp, u8p, i64]),
+    "gol_get_region": (ctypes.c_int, [vp, i64, i64, i64, i64, u8p]),
+    "gol_seed_dotnet": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int]),
+    "gol_seed_splitmix": (ctypes.c_int, [vp, u64]),
+    "gol_place_rle": (ctypes.c_int, [vp, ctypes.c_char_p, i64, i64]),
+    "gol_clear": (ctypes.c_int, [vp]),
+    "gol_step": (ctypes.c_int, [vp, i64]),
+    "gol_generation": (ctypes.c_int, [vp, i64p]),
+    "gol_synchronize": (ctypes.c_int, [vp]),
+    "gol_render_gray8": (ctypes.c_int, [vp, u8p, i64, ctypes.c_uint8]),
+    "gol_population": (ctypes.c_int, [vp, i64p]),
+    "gol_hash": (ctypes.c_int, [vp, u64p]),
+    "gol_info": (ctypes.c_int, [vp, i64p, i64p, ip, ip, ip]),
+    "gol_stream": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    "gol_last_error": (ctypes.c_char_p, []),
+    "gol_version": (ctypes.c_char_p, []),
+    "gol_strip_step": (ctypes.c_int, [sp, vp, vp, ctypes.c_int, i64, i64, vp]),
+    "gol_strip_seed_splitmix": (ctypes.c_int, [sp, vp, u64, vp]),
+    "gol_strip_pack": (ctypes.c_int, [sp, vp, vp, vp]),
+    "gol_strip_unpack": (ctypes.c_int, [sp, vp, vp, i64, ctypes.c_uint8, vp]),
+    "gol_strip_population": (ctypes.c_int, [sp, vp, vp, vp]),
+    "gol_strip_hash_partial": (ctypes.c_int, [sp, vp, vp, vp]),
+    "gol_hash_finalize": (u64, [u64, i64, i64]),
+    "gol_strip_plan": (ctypes.c_int, [sp, ctypes.c_int, i64, i64, i64p, i64p]),
+}
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libgol_hip.so; raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GolError(
+            f"{path} not found: build it with `python -m gameoflifewithactors_amd.build` "
+            "(there is no CPU fallback for the hot path)"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == GOL_OK:
+        return
+    msg = load().gol_last_error().decode(errors="replace")
+    exc = _ERRORS.get(rc, GolError)
+    raise exc(f"{what}: {msg} (code {rc})" if what else f"{msg} (code {rc})")

@@ -1,0 +1,138 @@
+"""Board: the GPU engine that replaces the reference's dictionary of cell actors.
+
+Reference seam: ``cells : IDictionary<int*int, CellRef>`` built from ``createCell`` in
+``GameOfLife/GameOfLife/GameOfLifeDriver.fs:16-30`` (Akka: ``GameofLife.fs:148-163``).  One ``Board``
+holds the whole grid in HBM (bit-packed when the width is a multiple of 32) and ``step(1)`` is one
+``updateView()`` tick (``GameOfLifeDriver.fs:32-34``) -- computed by the HIP kernels in
+``csrc/gol_kernels.hip`` through the C ABI in ``include/gol/gol.h``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import BOUNDED, INIT_DOTNET_MOD2, INIT_DOTNET_NEXT2, TORUS, check
+
+__all__ = ["Board", "TORUS", "BOUNDED", "INIT_DOTNET_MOD2", "INIT_DOTNET_NEXT2", "hash_finalize"]
+
+
+def _u8p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def hash_finalize(partial_sum: int, width: int, height: int) -> int:
+    return int(_lib.load().gol_hash_finalize(partial_sum & 0xFFFFFFFFFFFFFFFF, width, height))
+
+
+class Board:
+    """A width x height Life board on the current HIP device.
+
+    boundary: ``TORUS`` (the actors' topology, GameOfLifeDriver.fs:25) or ``BOUNDED`` (Script.fsx:11).
+    tblock_k: generations fused per kernel pass (0 = library default).
+    """
+
+    def __init__(self, width: int, height: int, boundary: int = TORUS, tblock_k: int = 0, num_gpus: int = 1):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._lib.gol_create(width, height, boundary, num_gpus, tblock_k, ctypes.byref(h)), "gol_create")
+        self._h = h
+        self.width, self.height, self.boundary = width, height, boundary
+
+    # ---------------------------------------------------------------- lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            check(self._lib.gol_destroy(self._h), "gol_destroy")
+            self._h = None
+
+    def __enter__(self) -> "Board":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- I/O
+    def set_cells(self, cells) -> "Board":
+        a = np.ascontiguousarray(np.asarray(cells, dtype=np.uint8)).reshape(-1)
+        check(self._lib.gol_set_cells(self._h, _u8p(a), a.size), "gol_set_cells")
+        return self
+
+    def get_cells(self) -> np.ndarray:
+        out = np.empty((self.height, self.width), dtype=np.uint8)
+        check(self._lib.gol_get_cells(self._h, _u8p(out), out.size), "gol_get_cells")
+        return out
+
+    def get_region(self, x: int, y: int, w: int, h: int) -> np.ndarray:
+        """Window of the board as a (h, w) uint8 array (must lie inside the board)."""
+        out = np.empty((h, w), dtype=np.uint8)
+        check(self._lib.gol_get_region(self._h, x, y, w, h, _u8p(out)), "gol_get_region")
+        return out
+
+    def render_gray8(self, alive_value: int = 128, stride: int | None = None) -> np.ndarray:
+        """Gray8 frame, pixels[x + y*stride] (GameOfLifeUI.fs:24-28: 128 for actors, 255 for Script.fsx)."""
+        stride = self.width if stride is None else stride
+        out = np.empty(stride * self.height, dtype=np.uint8)
+        check(self._lib.gol_render_gray8(self._h, _u8p(out), stride, alive_value), "gol_render_gray8")
+        return out
+
+    # ---------------------------------------------------------------- seeding
+    def seed_dotnet(self, seed: int, mode: int = INIT_DOTNET_MOD2) -> "Board":
+        check(self._lib.gol_seed_dotnet(self._h, seed, mode), "gol_seed_dotnet")
+        return self
+
+    def seed_splitmix(self, seed: int) -> "Board":
+        check(self._lib.gol_seed_splitmix(self._h, seed & 0xFFFFFFFFFFFFFFFF), "gol_seed_splitmix")
+        return self
+
+    def place_rle(self, rle: str, x: int, y: int) -> "Board":
+        check(self._lib.gol_place_rle(self._h, rle.encode(), x, y), "gol_place_rle")
+        return self
+
+    def clear(self) -> "Board":
+        check(self._lib.gol_clear(self._h), "gol_clear")
+        return self
+
+    # ---------------------------------------------------------------- stepping
+    def step(self, generations: int = 1) -> "Board":
+        check(self._lib.gol_step(self._h, generations), "gol_step")
+        return self
+
+    def synchronize(self) -> None:
+        check(self._lib.gol_synchronize(self._h), "gol_synchronize")
+
+    @property
+    def generation(self) -> int:
+        v = ctypes.c_int64()
+        check(self._lib.gol_generation(self._h, ctypes.byref(v)), "gol_generation")
+        return v.value
+
+    # ---------------------------------------------------------------- observables
+    def population(self) -> int:
+        v = ctypes.c_int64()
+        check(self._lib.gol_population(self._h, ctypes.byref(v)), "gol_population")
+        return v.value
+
+    def hash(self) -> int:
+        v = ctypes.c_uint64()
+        check(self._lib.gol_hash(self._h, ctypes.byref(v)), "gol_hash")
+        return v.value
+
+    def info(self) -> dict:
+        w, h = ctypes.c_int64(), ctypes.c_int64()
+        b, k, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self._lib.gol_info(self._h, *(ctypes.byref(x) for x in (w, h, b, k, p))), "gol_info")
+        return {"width": w.value, "height": h.value, "boundary": b.value, "tblock_k": k.value, "packed": bool(p.value)}
+
+    @property
+    def stream(self) -> int:
+        """The hipStream_t the board's kernels are launched on (as an integer handle)."""
+        s = ctypes.c_void_p()
+        check(self._lib.gol_stream(self._h, ctypes.byref(s)), "gol_stream")
+        return s.value or 0

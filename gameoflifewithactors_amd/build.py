@@ -1,0 +1,74 @@
+"""Build recipe for libgol_hip.so (gfx950) -- explicit hipcc, in-tree, no JIT cache.
+
+``python -m gameoflifewithactors_amd.build`` or ``__graft_entry__.build()``.  The shared library lands
+next to this file so it travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libgol_hip.so")
+SOURCES = [os.path.join(CSRC, "gol_kernels.hip"), os.path.join(CSRC, "gol_capi.cpp")]
+HEADERS = [
+    os.path.join(CSRC, "gol_bitlogic.h"),
+    os.path.join(CSRC, "gol_internal.h"),
+    os.path.join(ROOT, "include", "gol", "gol.h"),
+]
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    return "hipcc"
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    deps = SOURCES + HEADERS + [os.path.abspath(__file__)]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [
+            _hipcc(),
+            f"--offload-arch={ARCH}",
+            "-O3",
+            "-std=c++17",
+            "-fPIC",
+            "-Wall",
+            "-x",
+            "hip",
+            "-I",
+            os.path.join(ROOT, "include"),
+            "-c",
+            src,
+            "-o",
+            obj,
+        ]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

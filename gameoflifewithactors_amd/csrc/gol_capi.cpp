@@ -1,0 +1,653 @@
+// gol_capi.cpp -- the C ABI (include/gol/gol.h): board handles, seeding, stepping, readback.
+//
+// This file is the native runtime around the kernels: it owns device memory, picks the kernel
+// (bit-packed streaming step when width % 32 == 0, byte-per-cell step otherwise), splits a request
+// for N generations into temporal-blocked passes, and maps every HIP failure to a GOL_ERR_* code with a
+// thread-local message.  No C++ exception escapes an extern "C" function.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gol/gol.h"
+#include "gol_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define GOL_HIP(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return fail(GOL_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------- .NET Framework System.Random
+// Product restatement used by gol_seed_dotnet (GameOfLifeDriver.fs:10-11, GameofLife.fs:141-142,
+// Script.fsx:25,27): Knuth subtractive generator, MSEED 161803398, 56-entry table, inext/inextp 0/21.
+class DotNetRandom {
+   public:
+    explicit DotNetRandom(int32_t seed) {
+        const int32_t mbig = 2147483647;
+        int32_t sub = (seed == INT32_MIN) ? mbig : std::abs(seed);
+        int32_t mj = 161803398 - sub, mk = 1;
+        table_[55] = mj;
+        for (int i = 1; i < 55; i++) {
+            int ii = (21 * i) % 55;
+            table_[ii] = mk;
+            mk = (int32_t)((uint32_t)mj - (uint32_t)mk);
+            if (mk < 0) mk += mbig;
+            mj = table_[ii];
+        }
+        for (int k = 1; k < 5; k++)
+            for (int i = 1; i < 56; i++) {
+                table_[i] = (int32_t)((uint32_t)table_[i] - (uint32_t)table_[1 + (i + 30) % 55]);
+                if (table_[i] < 0) table_[i] += mbig;
+            }
+    }
+    int32_t Next() { return sample(); }
+    int32_t Next(int32_t max_value) { return (int32_t)(sample() * (1.0 / 2147483647) * max_value); }
+
+   private:
+    int32_t sample() {
+        if (++inext_ >= 56) inext_ = 1;
+        if (++inextp_ >= 56) inextp_ = 1;
+        int32_t r = (int32_t)((uint32_t)table_[inext_] - (uint32_t)table_[inextp_]);
+        if (r == 2147483647) r--;
+        if (r < 0) r += 2147483647;
+        table_[inext_] = r;
+        return r;
+    }
+    int32_t table_[56] = {0};
+    int inext_ = 0, inextp_ = 21;
+};
+
+// ---------------------------------------------------------------- RLE (Life run-length encoding)
+bool parse_rle(const char* p, std::vector<std::pair<int64_t, int64_t>>& out, std::string& err) {
+    if (!p) {
+        err = "null RLE";
+        return false;
+    }
+    // skip '#' comment lines and the "x = .., y = .." header line
+    for (;;) {
+        while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n') p++;
+        if (*p == '#' || *p == 'x') {
+            while (*p && *p != '\n') p++;
+            continue;
+        }
+        break;
+    }
+    int64_t dx = 0, dy = 0, count = 0;
+    for (; *p && *p != '!'; p++) {
+        const char c = *p;
+        if (c >= '0' && c <= '9') {
+            count = count * 10 + (c - '0');
+            if (count > (int64_t)1 << 40) {
+                err = "RLE run length too large";
+                return false;
+            }
+            continue;
+        }
+        if (c == ' ' || c == '\t' || c == '\r' || c == '\n') continue;
+        const int64_t n = count ? count : 1;
+        count = 0;
+        if (c == '$') {
+            dy += n;
+            dx = 0;
+        } else if (c == 'b' || c == '.') {
+            dx += n;
+        } else if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) {
+            for (int64_t i = 0; i < n; i++) out.emplace_back(dx + i, dy);
+            dx += n;
+        } else {
+            err = std::string("bad RLE character '") + c + "'";
+            return false;
+        }
+    }
+    return true;
+}
+
+__global__ void set_points_packed(uint32_t* words, int64_t pitch, const int64_t* xy, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t x = xy[2 * i], y = xy[2 * i + 1];
+    atomicOr(&words[y * pitch + x / 32], 1u << (x & 31));
+}
+
+__global__ void set_points_bytes(uint8_t* cells, int64_t W, const int64_t* xy, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    cells[xy[2 * i] + xy[2 * i + 1] * W] = 1;
+}
+
+int64_t pick_seg(int64_t out_rows, int64_t nstrips, int k) {
+    static const int64_t env_seg = [] {
+        const char* s = std::getenv("GOL_SEG_ROWS");
+        return s ? std::atoll(s) : 0LL;
+    }();
+    static const int64_t target_waves = [] {
+        const char* s = std::getenv("GOL_TARGET_WAVES");
+        return s ? std::atoll(s) : 4096LL;
+    }();
+    int64_t seg = env_seg > 0 ? env_seg : (out_rows * nstrips + target_waves - 1) / std::max<int64_t>(1, target_waves);
+    seg = std::max<int64_t>(seg, std::max<int64_t>(8 * (int64_t)k, 64));
+    return std::min<int64_t>(std::max<int64_t>(seg, 1), std::max<int64_t>(out_rows, 1));
+}
+
+bool valid_k(int k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 24 || k == 32; }
+
+int largest_k_at_most(int64_t n, int cap) {
+    static const int ks[] = {32, 24, 16, 8, 4, 2, 1};
+    for (int k : ks)
+        if (k <= cap && k <= n) return k;
+    return 1;
+}
+
+}  // namespace
+
+struct gol_board {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t W = 0, H = 0;
+    int boundary = GOL_TORUS;
+    int tblock = 16;
+    bool packed = false;
+    int64_t pitch = 0;  // words per row (packed)
+    void* buf[2] = {nullptr, nullptr};
+    int cur = 0;
+    unsigned long long* acc = nullptr;  // device scratch accumulator
+    int64_t generation = 0;
+
+    size_t bytes() const { return packed ? (size_t)(pitch * H) * 4 : (size_t)(W * H); }
+    uint32_t* words(int i) { return static_cast<uint32_t*>(buf[i]); }
+    uint8_t* cells(int i) { return static_cast<uint8_t*>(buf[i]); }
+
+    gol::StreamArgs stream_args(int64_t out_begin, int64_t out_end, int k) const {
+        gol::StreamArgs a{};
+        a.words = W / 32;
+        a.pitch = pitch;
+        a.rows = H;
+        a.ghost = 0;
+        a.y0 = 0;
+        a.height = H;
+        a.out_begin = out_begin;
+        a.out_end = out_end;
+        a.seg = pick_seg(out_end - out_begin, gol::stream_strips(a.words), k);
+        return a;
+    }
+};
+
+namespace {
+
+int check_board(gol_board* b) {
+    if (!b) return fail(GOL_ERR_INVALID, "null board");
+    hipError_t e = hipSetDevice(b->device);
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    return GOL_OK;
+}
+
+int sync(gol_board* b) {
+    GOL_HIP(hipStreamSynchronize(b->stream));
+    return GOL_OK;
+}
+
+int set_cells_impl(gol_board* b, const uint8_t* host) {
+    const size_t n = (size_t)(b->W * b->H);
+    if (!b->packed) {
+        GOL_HIP(hipMemcpyAsync(b->cells(b->cur), host, n, hipMemcpyHostToDevice, b->stream));
+        return sync(b);
+    }
+    uint8_t* staging = nullptr;
+    hipError_t e = hipMalloc(&staging, n);
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, std::string("hipMalloc staging: ") + hipGetErrorString(e));
+    int rc = GOL_OK;
+    do {
+        e = hipMemcpyAsync(staging, host, n, hipMemcpyHostToDevice, b->stream);
+        if (e != hipSuccess) break;
+        e = gol::launch_pack(staging, b->words(b->cur), b->W, b->H, b->pitch, 0, b->stream);
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    if (e != hipSuccess) rc = fail(GOL_ERR_HIP, std::string("set_cells: ") + hipGetErrorString(e));
+    (void)hipFree(staging);
+    return rc;
+}
+
+int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
+    const size_t n = (size_t)(stride * b->H);
+    uint8_t* staging = nullptr;
+    hipError_t e = hipMalloc(&staging, n);
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, std::string("hipMalloc staging: ") + hipGetErrorString(e));
+    int rc = GOL_OK;
+    do {
+        if (stride != b->W) {
+            e = hipMemsetAsync(staging, 0, n, b->stream);
+            if (e != hipSuccess) break;
+        }
+        if (b->packed)
+            e = gol::launch_unpack(b->words(b->cur), staging, b->W, b->H, b->pitch, 0, stride, value, b->stream);
+        else
+            e = gol::launch_bytes_render(b->cells(b->cur), staging, b->W, b->H, stride, value, b->stream);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(host, staging, n, hipMemcpyDeviceToHost, b->stream);
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    if (e != hipSuccess) rc = fail(GOL_ERR_HIP, std::string("readback: ") + hipGetErrorString(e));
+    (void)hipFree(staging);
+    return rc;
+}
+
+int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
+    GOL_HIP(hipMemsetAsync(b->acc, 0, sizeof(unsigned long long), b->stream));
+    if (b->packed) {
+        if (hash)
+            GOL_HIP(gol::launch_hash_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, b->acc, b->stream));
+        else
+            GOL_HIP(gol::launch_popcount_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, b->acc, b->stream));
+    } else {
+        if (hash)
+            GOL_HIP(gol::launch_hash_bytes(b->cells(b->cur), b->W, b->H, b->acc, b->stream));
+        else
+            GOL_HIP(gol::launch_popcount_bytes(b->cells(b->cur), b->W * b->H, b->acc, b->stream));
+    }
+    unsigned long long v = 0;
+    GOL_HIP(hipMemcpyAsync(&v, b->acc, sizeof(v), hipMemcpyDeviceToHost, b->stream));
+    GOL_HIP(hipStreamSynchronize(b->stream));
+    *out = hash ? gol_hash_finalize(v, b->W, b->H) : (uint64_t)v;
+    return GOL_OK;
+}
+
+int step_impl(gol_board* b, int64_t gens) {
+    if (!b->packed) {
+        for (int64_t g = 0; g < gens; g++) {
+            GOL_HIP(gol::launch_bytes_step(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H,
+                                           b->boundary == GOL_BOUNDED, b->stream));
+            b->cur ^= 1;
+            b->generation++;
+        }
+        return GOL_OK;
+    }
+    while (gens > 0) {
+        const int k = largest_k_at_most(gens, b->tblock);
+        gol::StreamArgs a = b->stream_args(0, b->H, k);
+        GOL_HIP(gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, k, b->boundary == GOL_BOUNDED,
+                                        b->boundary == GOL_TORUS, b->stream));
+        b->cur ^= 1;
+        b->generation += k;
+        gens -= k;
+    }
+    return GOL_OK;
+}
+
+int place_points(gol_board* b, const std::vector<int64_t>& xy) {
+    const int64_t n = (int64_t)xy.size() / 2;
+    if (n == 0) return GOL_OK;
+    int64_t* d = nullptr;
+    hipError_t e = hipMalloc(&d, xy.size() * sizeof(int64_t));
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc points");
+    int rc = GOL_OK;
+    do {
+        e = hipMemcpyAsync(d, xy.data(), xy.size() * sizeof(int64_t), hipMemcpyHostToDevice, b->stream);
+        if (e != hipSuccess) break;
+        const unsigned grid = (unsigned)((n + 255) / 256);
+        if (b->packed)
+            hipLaunchKernelGGL(set_points_packed, dim3(grid), dim3(256), 0, b->stream, b->words(b->cur), b->pitch, d, n);
+        else
+            hipLaunchKernelGGL(set_points_bytes, dim3(grid), dim3(256), 0, b->stream, b->cells(b->cur), b->W, d, n);
+        e = hipGetLastError();
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    if (e != hipSuccess) rc = fail(GOL_ERR_HIP, std::string("place_points: ") + hipGetErrorString(e));
+    (void)hipFree(d);
+    return rc;
+}
+
+void free_board(gol_board* b) {
+    for (auto& p : b->buf)
+        if (p) (void)hipFree(p);
+    if (b->acc) (void)hipFree(b->acc);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+int check_strip(const gol_strip* s) {
+    if (!s) return fail(GOL_ERR_INVALID, "null strip");
+    if (s->width < 32 || s->width % 32) return fail(GOL_ERR_INVALID, "strip width must be a positive multiple of 32");
+    if (s->height < 3 || s->rows < 1 || s->y0 < 0 || s->y0 + s->rows > s->height)
+        return fail(GOL_ERR_INVALID, "strip rows outside the board");
+    if (s->pitch < s->width / 32) return fail(GOL_ERR_INVALID, "strip pitch smaller than the row");
+    if (s->ghost < 0) return fail(GOL_ERR_INVALID, "negative ghost");
+    if (s->boundary != GOL_TORUS && s->boundary != GOL_BOUNDED) return fail(GOL_ERR_INVALID, "bad boundary");
+    if (s->wrap_rows && (s->ghost != 0 || s->rows != s->height || s->y0 != 0))
+        return fail(GOL_ERR_INVALID, "wrap_rows requires the whole board in one strip with ghost = 0");
+    return GOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gol_last_error(void) { return g_last_error.c_str(); }
+
+const char* gol_version(void) { return "gol_hip 0.1 (gfx950)"; }
+
+uint64_t gol_hash_finalize(uint64_t h, int64_t width, int64_t height) {
+    auto fmix = [](uint64_t k) {
+        k ^= k >> 33;
+        k *= 0xff51afd7ed558ccdULL;
+        k ^= k >> 33;
+        k *= 0xc4ceb9fe1a85ec53ULL;
+        k ^= k >> 33;
+        return k;
+    };
+    return fmix(h ^ fmix((uint64_t)width * 0x100000001B3ULL + (uint64_t)height));
+}
+
+int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out) {
+    try {
+        if (!out) return fail(GOL_ERR_INVALID, "null out");
+        *out = nullptr;
+        if (width < 3 || height < 3)
+            return fail(GOL_ERR_INVALID, "width and height must be >= 3 (smaller tori alias neighbours)");
+        if (width > ((int64_t)1 << 40) || height > ((int64_t)1 << 40) || width * height > ((int64_t)1 << 42))
+            return fail(GOL_ERR_INVALID, "board too large");
+        if (boundary != GOL_TORUS && boundary != GOL_BOUNDED) return fail(GOL_ERR_INVALID, "bad boundary");
+        if (num_gpus != 1)
+            return fail(GOL_ERR_UNSUPPORTED, "num_gpus must be 1; multi-GPU runs use one process per GPU (gol_strip_*)");
+        if (tblock_k == 0) tblock_k = 16;
+        if (!valid_k(tblock_k)) return fail(GOL_ERR_INVALID, "tblock_k must be one of 1,2,4,8,16,24,32");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(GOL_ERR_NO_DEVICE, "no HIP device");
+        gol_board* b = new gol_board();
+        b->W = width;
+        b->H = height;
+        b->boundary = boundary;
+        b->tblock = tblock_k;
+        b->packed = (width % 32) == 0;
+        b->pitch = b->packed ? width / 32 : 0;
+        hipError_t e = hipGetDevice(&b->device);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            free_board(b);
+            return fail(GOL_ERR_HIP, std::string("stream: ") + hipGetErrorString(e));
+        }
+        for (auto& p : b->buf) {
+            e = hipMalloc(&p, b->bytes());
+            if (e != hipSuccess) {
+                free_board(b);
+                return fail(GOL_ERR_OOM, std::string("hipMalloc board: ") + hipGetErrorString(e));
+            }
+        }
+        e = hipMalloc(&b->acc, 64);
+        if (e == hipSuccess) e = hipMemsetAsync(b->buf[0], 0, b->bytes(), b->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(b->buf[1], 0, b->bytes(), b->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(b->stream);
+        if (e != hipSuccess) {
+            free_board(b);
+            return fail(GOL_ERR_HIP, std::string("init: ") + hipGetErrorString(e));
+        }
+        *out = b;
+        return GOL_OK;
+    } catch (const std::exception& ex) {
+        return fail(GOL_ERR_OOM, ex.what());
+    } catch (...) {
+        return fail(GOL_ERR_INVALID, "unknown exception");
+    }
+}
+
+int gol_destroy(gol_board* b) {
+    if (!b) return fail(GOL_ERR_INVALID, "null board");
+    (void)hipSetDevice(b->device);
+    (void)hipStreamSynchronize(b->stream);
+    free_board(b);
+    return GOL_OK;
+}
+
+int gol_set_cells(gol_board* b, const uint8_t* cells, int64_t len) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (!cells || len != b->W * b->H) return fail(GOL_ERR_INVALID, "cells length must be width*height");
+    return set_cells_impl(b, cells);
+}
+
+int gol_get_cells(gol_board* b, uint8_t* cells, int64_t len) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (!cells || len != b->W * b->H) return fail(GOL_ERR_INVALID, "cells length must be width*height");
+    return readback_impl(b, cells, b->W, 1);
+}
+
+int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (!out || x < 0 || y < 0 || w < 0 || h < 0 || x + w > b->W || y + h > b->H)
+        return fail(GOL_ERR_INVALID, "region outside the board");
+    if (w == 0 || h == 0) return GOL_OK;
+    uint8_t* staging = nullptr;
+    hipError_t e = hipMalloc(&staging, (size_t)(w * h));
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc region");
+    do {
+        e = gol::launch_region(b->buf[b->cur], b->packed, b->W, b->pitch, x, y, w, h, staging, b->stream);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(out, staging, (size_t)(w * h), hipMemcpyDeviceToHost, b->stream);
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    (void)hipFree(staging);
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("get_region: ") + hipGetErrorString(e));
+    return GOL_OK;
+}
+
+int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t alive_value) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (!pixels || stride < b->W) return fail(GOL_ERR_INVALID, "stride must be >= width");
+    return readback_impl(b, pixels, stride, alive_value);
+}
+
+int gol_seed_dotnet(gol_board* b, int32_t seed, int mode) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (mode != GOL_INIT_DOTNET_MOD2 && mode != GOL_INIT_DOTNET_NEXT2) return fail(GOL_ERR_INVALID, "bad mode");
+    try {
+        std::vector<uint8_t> cells((size_t)(b->W * b->H));
+        DotNetRandom r(seed);
+        // creation order x outer, y inner (GameOfLifeDriver.fs:16-19; Array2D.init in Script.fsx:27)
+        for (int64_t x = 0; x < b->W; x++)
+            for (int64_t y = 0; y < b->H; y++)
+                cells[(size_t)(x + y * b->W)] = (mode == GOL_INIT_DOTNET_MOD2) ? (r.Next() % 2 == 0) : (r.Next(2) == 0);
+        b->generation = 0;
+        return set_cells_impl(b, cells.data());
+    } catch (const std::exception& ex) {
+        return fail(GOL_ERR_OOM, ex.what());
+    }
+}
+
+int gol_seed_splitmix(gol_board* b, uint64_t seed) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (b->packed)
+        GOL_HIP(gol::launch_splitmix_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, seed, b->stream));
+    else
+        GOL_HIP(gol::launch_splitmix_bytes(b->cells(b->cur), b->W, b->H, seed, b->stream));
+    b->generation = 0;
+    return sync(b);
+}
+
+int gol_clear(gol_board* b) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    GOL_HIP(hipMemsetAsync(b->buf[b->cur], 0, b->bytes(), b->stream));
+    b->generation = 0;
+    return sync(b);
+}
+
+int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    try {
+        std::vector<std::pair<int64_t, int64_t>> pts;
+        std::string err;
+        if (!parse_rle(rle, pts, err)) return fail(GOL_ERR_INVALID, err);
+        std::vector<int64_t> xy;
+        xy.reserve(pts.size() * 2);
+        for (auto& p : pts) {
+            xy.push_back((((x + p.first) % b->W) + b->W) % b->W);
+            xy.push_back((((y + p.second) % b->H) + b->H) % b->H);
+        }
+        return place_points(b, xy);
+    } catch (const std::exception& ex) {
+        return fail(GOL_ERR_OOM, ex.what());
+    }
+}
+
+int gol_step(gol_board* b, int64_t generations) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    if (generations < 0) return fail(GOL_ERR_INVALID, "negative generations");
+    return step_impl(b, generations);
+}
+
+int gol_generation(gol_board* b, int64_t* out) {
+    if (!b || !out) return fail(GOL_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(b->mu);
+    *out = b->generation;
+    return GOL_OK;
+}
+
+int gol_synchronize(gol_board* b) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    return sync(b);
+}
+
+int gol_population(gol_board* b, int64_t* out) {
+    if (int rc = check_board(b)) return rc;
+    if (!out) return fail(GOL_ERR_INVALID, "null out");
+    std::lock_guard<std::mutex> g(b->mu);
+    uint64_t v = 0;
+    if (int rc = reduce_impl(b, false, &v)) return rc;
+    *out = (int64_t)v;
+    return GOL_OK;
+}
+
+int gol_hash(gol_board* b, uint64_t* out) {
+    if (int rc = check_board(b)) return rc;
+    if (!out) return fail(GOL_ERR_INVALID, "null out");
+    std::lock_guard<std::mutex> g(b->mu);
+    return reduce_impl(b, true, out);
+}
+
+int gol_info(gol_board* b, int64_t* width, int64_t* height, int* boundary, int* tblock_k, int* packed) {
+    if (!b) return fail(GOL_ERR_INVALID, "null board");
+    if (width) *width = b->W;
+    if (height) *height = b->H;
+    if (boundary) *boundary = b->boundary;
+    if (tblock_k) *tblock_k = b->tblock;
+    if (packed) *packed = b->packed ? 1 : 0;
+    return GOL_OK;
+}
+
+int gol_stream(gol_board* b, void** stream) {
+    if (!b || !stream) return fail(GOL_ERR_INVALID, "null argument");
+    *stream = (void*)b->stream;
+    return GOL_OK;
+}
+
+// ---------------------------------------------------------------- row strips
+int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows) {
+    if (int rc = check_strip(s)) return rc;
+    if (!valid_k(k)) return fail(GOL_ERR_INVALID, "k must be one of 1,2,4,8,16,24,32");
+    const int64_t nstrips = gol::stream_strips(s->width / 32);
+    const int64_t seg = pick_seg(out_end - out_begin, nstrips, k);
+    if (seg_rows) *seg_rows = seg;
+    if (waves) *waves = nstrips * ((out_end - out_begin + seg - 1) / seg);
+    return GOL_OK;
+}
+
+int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin,
+                   int64_t out_end, void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
+    if (!valid_k(k)) return fail(GOL_ERR_INVALID, "k must be one of 1,2,4,8,16,24,32");
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    if (out_begin == out_end) return GOL_OK;
+    if (!s->wrap_rows) {
+        // every row the pass can read must exist in the buffer, except rows beyond a bounded board's edge
+        int64_t lo = out_begin - k, hi = out_end + k;
+        if (s->boundary == GOL_BOUNDED) {
+            lo = std::max<int64_t>(lo, -s->y0);
+            hi = std::min<int64_t>(hi, s->height - s->y0);
+        }
+        if (lo < -s->ghost || hi > s->rows + s->ghost)
+            return fail(GOL_ERR_INVALID, "pass reads rows outside the buffer: ghost must be >= k");
+    }
+    gol::StreamArgs a{};
+    a.words = s->width / 32;
+    a.pitch = s->pitch;
+    a.rows = s->rows;
+    a.ghost = s->ghost;
+    a.y0 = s->y0;
+    a.height = s->height;
+    a.out_begin = out_begin;
+    a.out_end = out_end;
+    a.seg = pick_seg(out_end - out_begin, gol::stream_strips(a.words), k);
+    GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0,
+                                    (hipStream_t)stream));
+    return GOL_OK;
+}
+
+int gol_strip_seed_splitmix(const gol_strip* s, uint32_t* buf, uint64_t seed, void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!buf) return fail(GOL_ERR_INVALID, "null buffer");
+    GOL_HIP(gol::launch_splitmix_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost, s->y0, seed,
+                                        (hipStream_t)stream));
+    return GOL_OK;
+}
+
+int gol_strip_pack(const gol_strip* s, const uint8_t* dev_cells, uint32_t* buf, void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!dev_cells || !buf) return fail(GOL_ERR_INVALID, "null buffer");
+    GOL_HIP(gol::launch_pack(dev_cells, buf, s->width, s->rows, s->pitch, s->ghost, (hipStream_t)stream));
+    return GOL_OK;
+}
+
+int gol_strip_unpack(const gol_strip* s, const uint32_t* buf, uint8_t* dev_cells, int64_t stride, uint8_t value,
+                     void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!dev_cells || !buf || stride < s->width) return fail(GOL_ERR_INVALID, "bad buffer or stride");
+    GOL_HIP(gol::launch_unpack(buf, dev_cells, s->width, s->rows, s->pitch, s->ghost, stride, value,
+                               (hipStream_t)stream));
+    return GOL_OK;
+}
+
+int gol_strip_population(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!buf || !dev_acc) return fail(GOL_ERR_INVALID, "null buffer");
+    GOL_HIP(gol::launch_popcount_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost,
+                                        (unsigned long long*)dev_acc, (hipStream_t)stream));
+    return GOL_OK;
+}
+
+int gol_strip_hash_partial(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream) {
+    if (int rc = check_strip(s)) return rc;
+    if (!buf || !dev_acc) return fail(GOL_ERR_INVALID, "null buffer");
+    GOL_HIP(gol::launch_hash_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost, s->y0,
+                                    (unsigned long long*)dev_acc, (hipStream_t)stream));
+    return GOL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// gol_internal.h -- launcher prototypes shared by gol_kernels.hip and gol_capi.cpp (not installed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gol {
+
+// Geometry of one streaming pass over a bit-packed buffer (see gol_kernels.hip).
+struct StreamArgs {
+    int64_t words;      // board words per row (board width / 32)
+    int64_t pitch;      // words per buffer row
+    int64_t rows;       // owned rows (in wrap mode: all rows of the buffer)
+    int64_t ghost;      // halo rows stored above and below the owned rows (0 in wrap mode)
+    int64_t y0;         // global row index of owned row 0 (bounded masking, strips)
+    int64_t height;     // global board height
+    int64_t out_begin;  // owned rows [out_begin, out_end) are produced
+    int64_t out_end;
+    int64_t seg;        // rows per wave segment
+    int64_t nstrips;    // filled by the launcher
+    int64_t nsegs;      // filled by the launcher
+};
+
+int64_t stream_strips(int64_t words);
+hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
+                              hipStream_t s);
+hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s);
+hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                       hipStream_t s);
+hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                         int64_t stride, uint8_t value, hipStream_t s);
+hipError_t launch_region(const void* board, bool packed, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
+                          int64_t h, uint8_t* out, hipStream_t s);
+hipError_t launch_bytes_render(const uint8_t* cells, uint8_t* out, int64_t W, int64_t H, int64_t stride,
+                               uint8_t value, hipStream_t s);
+hipError_t launch_splitmix_packed(uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
+                                  int64_t gy0, uint64_t seed, hipStream_t s);
+hipError_t launch_splitmix_bytes(uint8_t* cells, int64_t W, int64_t H, uint64_t seed, hipStream_t s);
+hipError_t launch_popcount_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
+                                  unsigned long long* acc, hipStream_t s);
+hipError_t launch_popcount_bytes(const uint8_t* cells, int64_t n, unsigned long long* acc, hipStream_t s);
+hipError_t launch_hash_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
+                              int64_t gy0, unsigned long long* acc, hipStream_t s);
+hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s);
+
+}  // namespace gol

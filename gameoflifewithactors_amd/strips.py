@@ -1,0 +1,236 @@
+"""Row-strip decomposition of one board over N GPUs (one process per GPU) with halo exchange.
+
+The reference runs one process with W*H cell actors (GameOfLifeDriver.fs:16-34); its only notion of
+"neighbour exchange" is the 8 State / NeighbourState messages per cell (GameOfLifeLogic.fs:47-58).
+Here rank r owns the global rows [y0_r, y0_r + rows_r) of a bit-packed board in HBM, plus `k` ghost
+rows above and below.  One pass advances k generations:
+
+    1. send my top k owned rows to rank r-1 and my bottom k rows to rank r+1, receive their edge rows
+       into my ghost rows (torch.distributed point-to-point: NCCL = RCCL over xGMI on GPUs, gloo on CPU)
+    2. meanwhile compute the interior rows [k, rows-k), which need no ghost rows
+    3. wait for the exchange, then compute the boundary rows [0, k) and [rows-k, rows)
+
+Torus: ring neighbours (r +- 1) mod N.  Bounded: the end strips have no outer neighbour; rows beyond
+the board are dead at every generation (the kernel masks them).  With N = 1 the single strip uses the
+wrap-rows layout (no ghosts, one launch per pass).
+
+The compute itself goes through an *engine*; the product engine is `HipEngine` (the C ABI,
+gol_strip_* in include/gol/gol.h).  Tests may inject a CPU engine to exercise partitioning and the
+exchange protocol with gloo; the product path never falls back to one.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import BOUNDED, TORUS, Strip, check
+
+
+def partition(height: int, world: int, rank: int) -> tuple[int, int]:
+    """Rows owned by `rank`: balanced contiguous strips; returns (y0, rows)."""
+    base, extra = divmod(height, world)
+    rows = base + (1 if rank < extra else 0)
+    y0 = rank * base + min(rank, extra)
+    return y0, rows
+
+
+@dataclass
+class Geometry:
+    width: int
+    height: int
+    y0: int
+    rows: int
+    ghost: int
+    pitch: int
+    boundary: int
+    wrap_rows: bool
+
+    def strip(self) -> Strip:
+        return Strip(self.width, self.height, self.y0, self.rows, self.ghost, self.pitch, self.boundary,
+                     1 if self.wrap_rows else 0)
+
+    @property
+    def buffer_rows(self) -> int:
+        return self.rows + 2 * self.ghost
+
+
+class HipEngine:
+    """gol_strip_* through libgol_hip.so on the given CUDA(HIP) device.  No CPU fallback."""
+
+    def __init__(self, device: torch.device):
+        self.lib = _lib.load()
+        self.device = device
+
+    def alloc(self, geom: Geometry) -> torch.Tensor:
+        return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32, device=self.device)
+
+    def step(self, geom: Geometry, src: torch.Tensor, dst: torch.Tensor, k: int, out_begin: int, out_end: int,
+             stream: torch.cuda.Stream) -> None:
+        s = geom.strip()
+        check(self.lib.gol_strip_step(ctypes.byref(s), src.data_ptr(), dst.data_ptr(), k, out_begin, out_end,
+                                      stream.cuda_stream), "gol_strip_step")
+
+    def seed_splitmix(self, geom: Geometry, buf: torch.Tensor, seed: int, stream) -> None:
+        s = geom.strip()
+        check(self.lib.gol_strip_seed_splitmix(ctypes.byref(s), buf.data_ptr(), seed & 0xFFFFFFFFFFFFFFFF,
+                                               stream.cuda_stream), "gol_strip_seed_splitmix")
+
+    def reduce(self, geom: Geometry, buf: torch.Tensor, what: str, stream) -> torch.Tensor:
+        acc = torch.zeros(1, dtype=torch.int64, device=self.device)
+        s = geom.strip()
+        fn = self.lib.gol_strip_hash_partial if what == "hash" else self.lib.gol_strip_population
+        with torch.cuda.stream(stream):
+            acc.zero_()
+            check(fn(ctypes.byref(s), buf.data_ptr(), acc.data_ptr(), stream.cuda_stream), what)
+        return acc
+
+    def set_cells(self, geom: Geometry, buf: torch.Tensor, cells_u8: torch.Tensor, stream) -> None:
+        s = geom.strip()
+        dev = cells_u8.to(self.device).contiguous()
+        check(self.lib.gol_strip_pack(ctypes.byref(s), dev.data_ptr(), buf.data_ptr(), stream.cuda_stream),
+              "gol_strip_pack")
+        stream.synchronize()
+
+    def get_cells(self, geom: Geometry, buf: torch.Tensor, stream) -> torch.Tensor:
+        out = torch.empty((geom.rows, geom.width), dtype=torch.uint8, device=self.device)
+        s = geom.strip()
+        check(self.lib.gol_strip_unpack(ctypes.byref(s), buf.data_ptr(), out.data_ptr(), geom.width, 1,
+                                        stream.cuda_stream), "gol_strip_unpack")
+        stream.synchronize()
+        return out.cpu()
+
+
+class StripRunner:
+    """One rank's strip of a width x height board; `k` generations per pass."""
+
+    def __init__(self, width: int, height: int, boundary: int, k: int, rank: int = 0, world: int = 1,
+                 device: torch.device | None = None, engine=None, group=None):
+        if width % 32:
+            raise ValueError("row strips need width % 32 == 0 (bit-packed layout)")
+        if boundary not in (TORUS, BOUNDED):
+            raise ValueError("bad boundary")
+        self.width, self.height, self.boundary, self.k = width, height, boundary, k
+        self.rank, self.world, self.group = rank, world, group
+        y0, rows = partition(height, world, rank)
+        if world > 1 and rows < k:
+            raise ValueError(f"strip of {rows} rows is thinner than the temporal block k={k}")
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.engine = engine if engine is not None else HipEngine(self.device)
+        single = world == 1
+        self.geom = Geometry(width, height, y0, rows, 0 if single else k, width // 32, boundary,
+                             wrap_rows=single and boundary == TORUS)
+        self.bufs = [self.engine.alloc(self.geom), self.engine.alloc(self.geom)]
+        self.cur = 0
+        self.generation = 0
+        self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else _NullStream()
+        self.up = (rank - 1) % world if (boundary == TORUS or rank > 0) else None
+        self.down = (rank + 1) % world if (boundary == TORUS or rank < world - 1) else None
+
+    # ---------------------------------------------------------------- state
+    def seed_splitmix(self, seed: int) -> None:
+        self.engine.seed_splitmix(self.geom, self.bufs[self.cur], seed, self.compute_stream)
+        self.generation = 0
+
+    def set_cells(self, cells_owned) -> None:
+        """cells_owned: (rows, width) uint8 of this rank's owned rows."""
+        self.engine.set_cells(self.geom, self.bufs[self.cur], torch.as_tensor(cells_owned, dtype=torch.uint8),
+                              self.compute_stream)
+        self.generation = 0
+
+    def get_cells(self) -> torch.Tensor:
+        return self.engine.get_cells(self.geom, self.bufs[self.cur], self.compute_stream)
+
+    # ---------------------------------------------------------------- one pass
+    def _exchange(self, buf: torch.Tensor, k: int):
+        """Post the halo exchange of `k` rows; returns the request list (empty when N = 1)."""
+        if self.world == 1:
+            return []
+        g, h = self.geom.ghost, self.geom.rows
+        ops = []
+        if self.up is not None:  # my top rows -> up's bottom ghost; up's bottom rows -> my top ghost
+            ops.append(dist.P2POp(dist.isend, buf[g:g + k], self.up, self.group, tag=1))
+        if self.down is not None:
+            ops.append(dist.P2POp(dist.isend, buf[g + h - k:g + h], self.down, self.group, tag=2))
+        if self.down is not None:
+            ops.append(dist.P2POp(dist.irecv, buf[g + h:g + h + k], self.down, self.group, tag=1))
+        if self.up is not None:
+            ops.append(dist.P2POp(dist.irecv, buf[g - k:g], self.up, self.group, tag=2))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def step_pass(self, k: int | None = None) -> None:
+        """Advance k (default self.k) generations: exchange || interior, then boundary rows."""
+        k = self.k if k is None else k
+        src, dst = self.bufs[self.cur], self.bufs[self.cur ^ 1]
+        h = self.geom.rows
+        s = self.compute_stream
+        if self.world == 1:
+            self.engine.step(self.geom, src, dst, k, 0, h, s)
+        else:
+            with _stream_ctx(s):
+                reqs = self._exchange(src, k)
+            lo, hi = min(k, h), max(h - k, min(k, h))
+            self.engine.step(self.geom, src, dst, k, lo, hi, s)  # interior overlaps the exchange
+            with _stream_ctx(s):
+                for r in reqs:
+                    r.wait()  # compute stream waits for the received ghost rows
+            self.engine.step(self.geom, src, dst, k, 0, lo, s)
+            self.engine.step(self.geom, src, dst, k, hi, h, s)
+        self.cur ^= 1
+        self.generation += k
+
+    def step(self, generations: int) -> None:
+        while generations > 0:
+            k = self.k if generations >= self.k else _largest_k(generations)
+            self.step_pass(k)
+            generations -= k
+
+    def launches_per_pass(self) -> int:
+        return 1 if self.world == 1 else 3
+
+    def kernel_time_per_pass(self, total_s: float, passes: int) -> float:
+        return total_s / passes
+
+    # ---------------------------------------------------------------- observables (global)
+    def _reduce(self, what: str) -> int:
+        acc = self.engine.reduce(self.geom, self.bufs[self.cur], what, self.compute_stream)
+        if self.device.type == "cuda":
+            self.compute_stream.synchronize()
+        if self.world > 1:
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+        return int(acc.item()) & 0xFFFFFFFFFFFFFFFF
+
+    def population(self) -> int:
+        return self._reduce("population")
+
+    def hash(self) -> int:
+        return int(_lib.load().gol_hash_finalize(self._reduce("hash"), self.width, self.height))
+
+
+def _largest_k(n: int) -> int:
+    for k in (32, 24, 16, 8, 4, 2, 1):
+        if k <= n:
+            return k
+    return 1
+
+
+class _NullStream:
+    cuda_stream = 0
+
+    def synchronize(self):
+        pass
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _stream_ctx(s):
+    return torch.cuda.stream(s) if isinstance(s, torch.cuda.Stream) else _NullCtx()

@@ -1,0 +1,134 @@
+/*
+ * gol.h -- C ABI of the MI355X Game of Life engine (libgol_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path: the per-cell actors of
+ *   GameOfLife/GameOfLife/GameOfLifeLogic.fs:39-71   (MailboxProcessor cell, `createCell`)
+ *   GameOfLife/GameOfLifeAkka/GameofLife.fs:88-138   (Akka `CellAkka`, `ICell.Send`)
+ * and the dictionary of them built by the driver (GameOfLifeDriver.fs:16-30, GameofLife.fs:148-163).
+ * One board handle replaces the W*H cell actors; `gol_step(b, 1)` replaces one `updateView()` tick
+ * (GameOfLifeDriver.fs:32-34); `gol_render_gray8` / `gol_get_cells` replace the W*H `Update` posts
+ * consumed by the render agent (GameOfLifeUI.fs:21-31).  The F# P/Invoke declarations that bind each
+ * entry point are in INTEGRATION.md.
+ *
+ * Conventions: cdecl, plain pointers, int64_t sizes.  Every function returns 0 (GOL_OK) or a negative
+ * GOL_ERR_* code; gol_last_error() returns a thread-local message for the last failure on the calling
+ * thread.  No C++ exception crosses this ABI.  Host buffers are borrowed for the duration of the call
+ * only (P/Invoke pins blittable byte[] for the call).  Each board handle is serialised by an internal
+ * mutex (the reference's timer can re-enter updateView, GameOfLifeDriver.fs:38-40); separate handles are
+ * independent.  Cell layout for host buffers: one byte per cell, index x + y*width, nonzero = alive
+ * (GameOfLifeUI.fs:24-28 pixel order).
+ */
+#ifndef GOL_GOL_H
+#define GOL_GOL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOL_OK 0
+#define GOL_ERR_INVALID -1     /* bad argument, size or geometry */
+#define GOL_ERR_HIP -2         /* HIP runtime / kernel launch failure */
+#define GOL_ERR_OOM -3         /* device allocation failed */
+#define GOL_ERR_UNSUPPORTED -4 /* valid request this build does not implement */
+#define GOL_ERR_NO_DEVICE -5   /* no usable gfx950 device */
+
+enum { GOL_TORUS = 0, GOL_BOUNDED = 1 };
+/* gol_seed_dotnet modes */
+enum {
+    GOL_INIT_DOTNET_MOD2 = 0, /* GameOfLifeDriver.fs:9-11,16-19: x outer, y inner, Random.Next() % 2 = 0 */
+    GOL_INIT_DOTNET_NEXT2 = 1 /* Script.fsx:25-27: Array2D.init (x outer), Random.Next 2 = 0 */
+};
+
+typedef struct gol_board gol_board; /* opaque; library-owned */
+
+/* Replaces `cells = seq { for x .. for y .. createCell ... } |> dict` (GameOfLifeDriver.fs:16-19) and the
+ * neighbour wiring (L21-30).  width/height >= 3 (smaller tori alias neighbours: the reference's
+ * Dictionary never reaches 8 keys and the board freezes, GameOfLifeLogic.fs:58 -- rejected here).
+ * boundary: GOL_TORUS (actors, GameOfLifeDriver.fs:25) or GOL_BOUNDED (Script.fsx:11).
+ * num_gpus: must be 1 in this build (multi-GPU runs use one process per GPU, gol_strip_*).
+ * tblock_k: generations fused per pass (0 = default 16; one of 1,2,4,8,16,24,32).
+ * The initial board is all dead. */
+int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
+int gol_destroy(gol_board* b);
+
+/* Board I/O: cells[x + y*width], len == width*height.  Replaces createCell's `alive` argument
+ * (GameOfLifeLogic.fs:39) and, on readback, the per-cell Update(alive, location) stream (L64). */
+int gol_set_cells(gol_board* b, const uint8_t* cells, int64_t len);
+int gol_get_cells(gol_board* b, uint8_t* cells, int64_t len);
+/* Read a window (x, y, w, h) of the board (no wrap; must lie inside): out[i + j*w] = cell (x+i, y+j). */
+int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out);
+
+/* Seeding.  gol_seed_dotnet restates .NET Framework System.Random(seed) exactly as the reference uses it
+ * (GameOfLifeDriver.fs:9-11 with an explicit seed instead of DateTime.Now.Ticks).  gol_seed_splitmix is
+ * the build-owned device-side init for large boards.  gol_place_rle ORs a Life RLE pattern
+ * with its top-left at (x, y), wrapped modulo the board. */
+int gol_seed_dotnet(gol_board* b, int32_t seed, int mode);
+int gol_seed_splitmix(gol_board* b, uint64_t seed);
+int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y);
+int gol_clear(gol_board* b);
+
+/* Advance `generations` synchronous B3/S23 generations (GameOfLifeLogic.fs:47-66 under the Reset->State
+ * phase barrier).  Asynchronous with respect to the host; any readback synchronises. */
+int gol_step(gol_board* b, int64_t generations);
+int gol_generation(gol_board* b, int64_t* out);
+int gol_synchronize(gol_board* b);
+
+/* Replaces the render agent's pixel fill (GameOfLifeUI.fs:24-28; GameofLife.fs:53-57; Script.fsx:33-35):
+ * pixels[x + y*stride] = alive ? alive_value : 0, stride >= width, buffer >= stride*height bytes. */
+int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t alive_value);
+
+/* Observables for parity checks. */
+int gol_population(gol_board* b, int64_t* out);
+int gol_hash(gol_board* b, uint64_t* out); /* canonical 64-bit board hash */
+
+/* Introspection: width, height, boundary, tblock_k, packed (1 = bit-packed path, 0 = byte path). */
+int gol_info(gol_board* b, int64_t* width, int64_t* height, int* boundary, int* tblock_k, int* packed);
+/* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller. */
+int gol_stream(gol_board* b, void** stream);
+
+const char* gol_last_error(void);
+const char* gol_version(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * Row-strip entry points for multi-GPU runs (one process per GPU; the caller owns device memory and
+ * does the halo exchange, e.g. RCCL send/recv).  A strip buffer holds `ghost` halo rows, then `rows`
+ * owned rows (global rows [y0, y0+rows)), then `ghost` halo rows; each buffer row is `pitch` 32-bit
+ * words, of which the first width/32 are the board row (bit b of word w = cell x = 32w + b).
+ * width must be a multiple of 32.  With world size 1 a strip may instead set wrap_rows = 1, ghost = 0,
+ * rows = height: torus rows then wrap inside the buffer (the single-GPU board layout).
+ * `stream` is a hipStream_t (NULL = default stream).  All calls are asynchronous. */
+typedef struct gol_strip {
+    int64_t width;    /* global board width (cells) */
+    int64_t height;   /* global board height (rows) */
+    int64_t y0;       /* global row of owned row 0 */
+    int64_t rows;     /* owned rows */
+    int64_t ghost;    /* halo rows above and below (>= k for a k-generation pass unless wrap_rows) */
+    int64_t pitch;    /* words per buffer row (>= width/32) */
+    int32_t boundary; /* GOL_TORUS | GOL_BOUNDED */
+    int32_t wrap_rows;
+} gol_strip;
+
+/* k generations over owned rows [out_begin, out_end) from src to dst (distinct buffers, same geometry).
+ * Reads rows [out_begin-k, out_end+k); with wrap_rows = 0 those must lie in [-ghost, rows+ghost). */
+int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin,
+                   int64_t out_end, void* stream);
+int gol_strip_seed_splitmix(const gol_strip* s, uint32_t* buf, uint64_t seed, void* stream);
+/* cells: host or device bytes of the owned rows, cells[x + r*width] (r = owned row) */
+int gol_strip_pack(const gol_strip* s, const uint8_t* dev_cells, uint32_t* buf, void* stream);
+int gol_strip_unpack(const gol_strip* s, const uint32_t* buf, uint8_t* dev_cells, int64_t stride, uint8_t value,
+                     void* stream);
+/* Add this strip's population / canonical-hash partial sum into *dev_acc (device uint64). */
+int gol_strip_population(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream);
+int gol_strip_hash_partial(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream);
+/* Combine the (wrapping) sum of every strip's partial into the canonical board hash. */
+uint64_t gol_hash_finalize(uint64_t partial_sum, int64_t width, int64_t height);
+/* Number of wavefront column strips / rows per segment the step kernel uses (for roofline accounting). */
+int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves,
+                   int64_t* seg_rows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOL_GOL_H */

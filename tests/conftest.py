@@ -1,0 +1,32 @@
+"""Shared test setup.
+
+Markers: ``gpu`` -- needs a real MI355X (run with ``-m gpu`` on the GPU box); everything else runs on
+CPU.  The CPU oracle (``oracle/``) is test infrastructure: tests use it only as the checker.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(ROOT, "oracle")
+for p in (ROOT, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The numpy oracle twin, with the C restatement built (make -C oracle)."""
+    if not os.path.exists(os.path.join(ORACLE, "build", "libgol_oracle.so")) or not os.path.exists(
+        os.path.join(ORACLE, "build", "actor_protocol")
+    ):
+        subprocess.run(["make", "-C", ORACLE], check=True, stdout=subprocess.DEVNULL)
+    import gol_oracle
+
+    return gol_oracle

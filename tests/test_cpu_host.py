@@ -1,0 +1,138 @@
+"""CPU tests of the product's host side: the bit logic compiled for the host, the C ABI library's
+exports, its no-GPU error behaviour, and the Python mirror of the reference's F# types.
+No kernel is launched here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+HEADER = os.path.join(ROOT, "include", "gol", "gol.h")
+
+
+def test_bitlogic_exhaustive_on_host(tmp_path):
+    """gol_bitlogic.h (the kernel's 13-op rule) vs GameOfLifeLogic.fs:59-63 on all 3x3 neighbourhoods."""
+    exe = tmp_path / "test_bitlogic"
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(HERE, "cpp", "test_bitlogic.cpp"), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    assert '"mismatches": 0' in out
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(gol_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared_functions()
+    for must in ("gol_create", "gol_step", "gol_render_gray8", "gol_hash", "gol_strip_step", "gol_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from gameoflifewithactors_amd import _lib
+
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in _declared_functions():
+        assert hasattr(lib, name), f"libgol_hip.so does not export {name}"
+        assert name in _lib.SIGNATURES, f"_lib.SIGNATURES lacks a binding for {name}"
+
+
+def test_library_reports_version_without_gpu():
+    from gameoflifewithactors_amd import _lib
+
+    assert b"gfx950" in _lib.load().gol_version()
+
+
+def test_hash_finalize_matches_oracle(oracle):
+    """gol_hash_finalize is host code: the product's final mix equals the oracle's."""
+    from gameoflifewithactors_amd import hash_finalize
+
+    rng = np.random.default_rng(3)
+    b = (rng.random((9, 130)) < 0.5).astype(np.uint8)
+    # rebuild the oracle's partial sum and finalise it with the product
+    h, w = b.shape
+    nc = (w + 63) // 64
+    padded = np.zeros((h, nc * 64), np.uint8)
+    padded[:, :w] = b
+    v = np.packbits(padded.reshape(h, nc, 64), axis=2, bitorder="little").view("<u8").reshape(h, nc)
+    key = np.arange(h * nc, dtype=np.uint64).reshape(h, nc)
+    with np.errstate(over="ignore"):
+        acc = int(np.sum(oracle._fmix64(v.astype(np.uint64) ^ oracle._fmix64(key + np.uint64(0x9E3779B97F4A7C15))),
+                         dtype=np.uint64))
+    assert hash_finalize(acc, w, h) == oracle.board_hash(b)
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-GPU failure path")
+def test_create_fails_loudly_without_gpu():
+    from gameoflifewithactors_amd import Board
+
+    with pytest.raises(RuntimeError):
+        Board(64, 64)
+
+
+def test_invalid_arguments_rejected_before_device():
+    from gameoflifewithactors_amd import Board
+
+    with pytest.raises(ValueError):
+        Board(2, 100)  # < 3: the reference's Dictionary never reaches 8 keys (GameOfLifeLogic.fs:58)
+    with pytest.raises(ValueError):
+        Board(64, 64, boundary=7)
+    with pytest.raises(NotImplementedError):
+        Board(64, 64, num_gpus=2)
+    with pytest.raises(ValueError):
+        Board(64, 64, tblock_k=5)
+
+
+def test_strip_validation_without_gpu():
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    s = _lib.Strip(width=96, height=10, y0=0, rows=10, ghost=0, pitch=3, boundary=0, wrap_rows=0)
+    w, seg = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.gol_strip_plan(ctypes.byref(s), 4, 0, 10, ctypes.byref(w), ctypes.byref(seg)) == 0
+    assert w.value == 1 and seg.value == 10  # 3 words -> 1 column strip; 10 rows -> 1 segment
+    bad = _lib.Strip(width=100, height=10, y0=0, rows=10, ghost=0, pitch=4, boundary=0, wrap_rows=0)
+    assert lib.gol_strip_plan(ctypes.byref(bad), 4, 0, 10, None, None) == _lib.GOL_ERR_INVALID
+    # a k-generation pass needs k ghost rows when rows do not wrap
+    dummy = ctypes.c_void_p(16)
+    assert lib.gol_strip_step(ctypes.byref(s), dummy, ctypes.c_void_p(32), 4, 0, 10, None) == _lib.GOL_ERR_INVALID
+
+
+# ---------------------------------------------------------------- mirror of the F# types
+def test_logic_mirror():
+    from gameoflifewithactors_amd import logic
+
+    assert logic.grid == logic.Grid(100, 100) and logic.gridProduct == 10000
+    order = []
+    logic.apply_grid(lambda x, y: order.append((x, y)), logic.Grid(3, 2))
+    assert order == [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0), (2, 1)]  # x outer, y inner
+
+
+def test_update_agent_fills_pixels_like_the_reference():
+    from gameoflifewithactors_amd.driver import UpdateAgent
+    from gameoflifewithactors_amd.logic import Grid, Location, UpdateView
+
+    frames = []
+    agent = UpdateAgent(Grid(3, 2), 128, on_frame=lambda p: frames.append(p.copy()))
+    agent.post(UpdateView.Reset())
+    for x in range(3):
+        for y in range(2):
+            agent.post(UpdateView.Update((x + y) % 2 == 0, Location(x, y)))
+    assert len(frames) == 1
+    assert frames[0].tolist() == [128, 0, 128, 0, 128, 0]  # pixels[x + y*W]

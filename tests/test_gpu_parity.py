@@ -1,0 +1,267 @@
+"""GPU parity tests: the HIP path (through the C ABI, libgol_hip.so) against the CPU oracle.
+
+Bar: bit-exact boards (integer work).  Oracle = oracle/gol_oracle.{c,py} (test infrastructure).
+Sizes are chosen so the oracle finishes in seconds; full-size boards are checked through
+size-independent properties (windowed light-cone checks against the oracle, temporal-block
+invariance, hash/population consistency).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KS = [1, 2, 4, 8, 16, 24, 32]
+
+
+@pytest.fixture(scope="module")
+def gol():
+    import gameoflifewithactors_amd as g
+    from gameoflifewithactors_amd import _lib
+
+    _lib.load()
+    return g
+
+
+def _rand(h, w, seed, p=0.5):
+    return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
+
+
+# ---------------------------------------------------------------- small boards vs the oracle
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", [(32, 3), (64, 5), (96, 64), (128, 127), (320, 77), (2048, 40), (4000 + 96, 9)])
+def test_packed_step_matches_oracle(gol, oracle, boundary, w, h):
+    b0 = _rand(h, w, w * 1000 + h)
+    want = {1: oracle.c_run(b0, 1, boundary)}
+    want[37] = oracle.c_run(want[1], 36, boundary)
+    for k in KS:
+        with gol.Board(w, h, boundary, tblock_k=k) as b:
+            assert b.info()["packed"]
+            b.set_cells(b0)
+            assert np.array_equal(b.get_cells(), b0)
+            b.step(1)
+            assert np.array_equal(b.get_cells(), want[1]), f"k={k} gen 1"
+            b.step(36)
+            assert np.array_equal(b.get_cells(), want[37]), f"k={k} gen 37"
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", [(3, 3), (100, 100), (33, 7), (257, 40)])
+def test_byte_path_matches_oracle(gol, oracle, boundary, w, h):
+    b0 = _rand(h, w, w + 7 * h)
+    with gol.Board(w, h, boundary) as b:
+        assert not b.info()["packed"]
+        b.set_cells(b0)
+        b.step(25)
+        assert np.array_equal(b.get_cells(), oracle.c_run(b0, 25, boundary))
+
+
+@pytest.mark.parametrize("k", KS)
+def test_deep_pass_matches_oracle_many_generations(gol, oracle, k):
+    """One long run (K-blocked passes + remainder passes) against 150 oracle generations."""
+    b0 = _rand(96, 256, 99 + k, p=0.35)
+    for boundary in (0, 1):
+        with gol.Board(256, 96, boundary, tblock_k=k) as b:
+            b.set_cells(b0).step(150)
+            assert np.array_equal(b.get_cells(), oracle.c_run(b0, 150, boundary))
+
+
+def test_edge_cases(gol, oracle):
+    for boundary in (0, 1):
+        with gol.Board(64, 64, boundary) as b:  # empty board stays empty
+            b.step(100)
+            assert b.population() == 0
+        full = np.ones((8, 64), np.uint8)
+        with gol.Board(64, 8, boundary) as b:
+            b.set_cells(full).step(1)
+            assert np.array_equal(b.get_cells(), oracle.c_run(full, 1, boundary))
+    with gol.Board(64, 64) as b:
+        b.step(0)
+        assert b.generation == 0
+
+
+# ---------------------------------------------------------------- golden fixtures
+def _golden():
+    with open(os.path.join(HERE, "golden", "golden_small.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _setup(gol, b, case, oracle):
+    if case["init"] == "dotnet-mod2":
+        b.seed_dotnet(case["seed"], gol.INIT_DOTNET_MOD2)
+    elif case["init"] == "dotnet-next2":
+        b.seed_dotnet(case["seed"], gol.INIT_DOTNET_NEXT2)
+    elif case["init"] == "splitmix":
+        b.seed_splitmix(case["seed"])
+    else:
+        pats = {"gosper_gun": oracle.GOSPER_GUN, "r_pentomino": oracle.R_PENTOMINO}
+        for name, x, y in case["rle"]:
+            b.place_rle(pats[name], x, y)
+
+
+@pytest.mark.parametrize("name", sorted(_golden()))
+@pytest.mark.parametrize("k", [1, 16])
+def test_golden_fixtures(gol, oracle, name, k):
+    case = _golden()[name]
+    boards = np.load(os.path.join(HERE, "golden", "golden_boards.npz"))
+    bd = 0 if case["boundary"] == "torus" else 1
+    w, h = case["width"], case["height"]
+    with gol.Board(w, h, bd, tblock_k=k) as b:
+        _setup(gol, b, case, oracle)
+        done = 0
+        for cp in sorted(int(c) for c in case["checkpoints"]):
+            b.step(cp - done)
+            done = cp
+            want = case["checkpoints"][str(cp)]
+            assert str(b.hash()) == want["hash"], f"{name} gen {cp}"
+            assert b.population() == want["population"]
+            key = f"{name}_g{cp}"
+            if key in boards.files:
+                got = np.packbits(b.get_cells(), axis=None, bitorder="little")
+                assert np.array_equal(got, boards[key])
+
+
+# ---------------------------------------------------------------- observables / formats
+def test_hash_population_render_region(gol, oracle):
+    b0 = _rand(50, 320, 5)
+    with gol.Board(320, 50) as b:
+        b.set_cells(b0)
+        assert b.hash() == oracle.board_hash(b0)
+        assert b.population() == oracle.population(b0)
+        assert np.array_equal(b.render_gray8(128), oracle.render_gray8(b0, 128))
+        assert np.array_equal(b.render_gray8(255, stride=333), oracle.render_gray8(b0, 255, stride=333))
+        assert np.array_equal(b.get_region(17, 3, 100, 20), b0[3:23, 17:117])
+    with gol.Board(100, 30) as b:  # byte path
+        b0 = _rand(30, 100, 6)
+        b.set_cells(b0)
+        assert b.hash() == oracle.board_hash(b0) and b.population() == oracle.population(b0)
+        assert np.array_equal(b.render_gray8(128), oracle.render_gray8(b0, 128))
+
+
+@pytest.mark.parametrize("w,h", [(100, 100), (128, 64), (333, 9)])
+def test_seeding_matches_oracle(gol, oracle, w, h):
+    with gol.Board(w, h) as b:
+        for mode in (0, 1):
+            b.seed_dotnet(42, mode)
+            assert np.array_equal(b.get_cells(), oracle.seed_dotnet(w, h, 42, mode))
+        b.seed_splitmix(0x5EED)
+        assert np.array_equal(b.get_cells(), oracle.seed_splitmix(w, h, 0x5EED))
+
+
+def test_place_rle_wraps(gol, oracle):
+    with gol.Board(64, 64) as b:
+        b.place_rle(oracle.GOSPER_GUN, 50, 60)
+        want = oracle.place_rle(np.zeros((64, 64), np.uint8), oracle.GOSPER_GUN, 50, 60)
+        assert np.array_equal(b.get_cells(), want)
+    with gol.Board(64, 64) as b, pytest.raises(ValueError):
+        b.place_rle("3o?", 0, 0)
+
+
+# ---------------------------------------------------------------- known answers at larger sizes
+def test_glider_period_on_large_torus(gol, oracle):
+    w = 4096
+    with gol.Board(w, 64) as b:
+        b.place_rle(oracle.GLIDER, 100, 20)
+        h0 = b.hash()
+        b.step(4 * 64)  # vertical period 4H moves it 64 cells right, not yet home
+        assert b.hash() != h0 and b.population() == 5
+    with gol.Board(256, 256) as b:
+        b.place_rle(oracle.GLIDER, 7, 9)
+        h0 = b.hash()
+        b.step(4 * 256)
+        assert b.hash() == h0
+
+
+def test_r_pentomino_1103(gol, oracle):
+    for k in (1, 16, 32):
+        with gol.Board(1024, 1024, gol.BOUNDED, tblock_k=k) as b:
+            b.place_rle(oracle.R_PENTOMINO, 511, 511)
+            b.step(1103)
+            assert b.population() == 116
+
+
+def test_gosper_gun_long_run_bounded(gol, oracle):
+    # bounded 256^2 (Script.fsx:26 board size) gun + R-pentomino, 5000 generations vs the oracle
+    b0 = np.zeros((256, 256), np.uint8)
+    oracle.place_rle(b0, oracle.GOSPER_GUN, 10, 10)
+    oracle.place_rle(b0, oracle.R_PENTOMINO, 180, 150)
+    want = oracle.c_run(b0, 5000, 1)
+    with gol.Board(256, 256, gol.BOUNDED) as b:
+        b.set_cells(b0).step(5000)
+        assert np.array_equal(b.get_cells(), want)
+
+
+# ---------------------------------------------------------------- full-size properties
+def _wrapped_region(b, n, x0, y0, ww, wh):
+    """Read a window that may wrap around the torus (split into at most 4 in-board regions)."""
+    out = np.zeros((wh, ww), np.uint8)
+    xs = [(x0, min(ww, n - x0), 0)] + ([(0, ww - (n - x0), n - x0)] if x0 + ww > n else [])
+    ys = [(y0, min(wh, n - y0), 0)] + ([(0, wh - (n - y0), n - y0)] if y0 + wh > n else [])
+    for (xa, w, ox) in xs:
+        for (ya, h, oy) in ys:
+            out[oy:oy + h, ox:ox + w] = b.get_region(xa, ya, w, h)
+    return out
+
+
+def test_65536_window_light_cone(gol, oracle):
+    """65536^2 torus, splitmix seed, 64 generations: windows of the GPU board equal the oracle run on
+    each window grown by the light cone (64 cells per side) -- exact at any board size."""
+    n, gens, seed = 65536, 64, 0x5EED
+    ww, wh = 160, 96
+    with gol.Board(n, n, tblock_k=16) as b:
+        b.seed_splitmix(seed)
+        b.step(gens)
+        for (x0, y0) in ((1000, 2000), (n - 150, 4000), (30000, n - 40), (n - 10, n - 10)):
+            xs = (np.arange(x0 - gens, x0 + ww + gens)) % n
+            ys = (np.arange(y0 - gens, y0 + wh + gens)) % n
+            init = _splitmix_window(seed, n, xs, ys)
+            # a bounded run is exact inside the cone: the window's edges never reach the interior
+            want = oracle.c_run(init, gens, 1)[gens:gens + wh, gens:gens + ww]
+            assert np.array_equal(_wrapped_region(b, n, x0, y0, ww, wh), want), (x0, y0)
+
+
+def _splitmix_window(seed, width, xs, ys):
+    wc = (width + 31) // 32
+    chunk = ys[:, None].astype(np.uint64) * np.uint64(wc) + (xs[None, :] // 32).astype(np.uint64)
+    import gol_oracle as o
+
+    bits = (o._splitmix64(chunk ^ np.uint64(seed)) & np.uint64(0xFFFFFFFF))
+    return ((bits >> (xs[None, :] % 32).astype(np.uint64)) & np.uint64(1)).astype(np.uint8)
+
+
+def test_65536_temporal_block_invariance(gol):
+    """The same 65536^2 run at every K gives the same board (hash + population)."""
+    n = 65536
+    res = {}
+    with gol.Board(n, n, tblock_k=1) as ref:
+        ref.seed_splitmix(7)
+        ref.step(48)
+        res[1] = (ref.hash(), ref.population())
+    for k in (8, 16, 32):
+        with gol.Board(n, n, tblock_k=k) as b:
+            b.seed_splitmix(7)
+            b.step(48)
+            res[k] = (b.hash(), b.population())
+    assert len(set(res.values())) == 1, res
+
+
+# ---------------------------------------------------------------- driver mirror on the GPU
+def test_driver_update_view_matches_oracle(gol, oracle):
+    from gameoflifewithactors_amd import driver
+
+    frames = []
+    agent = driver.UpdateAgent(on_frame=lambda p: frames.append(p.copy()))
+    with driver.run(seed=42, agent=agent) as game:
+        for _ in range(3):
+            game.update_view()
+    b = oracle.seed_dotnet(100, 100, 42, 0)
+    for i in range(3):
+        b = oracle.step(b, 0)
+        assert np.array_equal(frames[i], oracle.render_gray8(b, 128))
+    fast = driver.UpdateAgent(on_frame=lambda p: frames.append(p.copy()))
+    with driver.run(seed=42, agent=fast, emit="pixels") as game:
+        game.update_view()
+    assert np.array_equal(frames[-1], frames[0])

@@ -1,0 +1,189 @@
+"""CPU tests: pin the oracle (oracle/) before trusting it.
+
+The reference holds no tests or fixtures for this path, so the pins are:
+* published .NET Framework System.Random values (the reference's RNG, GameOfLifeDriver.fs:10-11);
+* Life known answers (blinker, block, full board, glider period, Gosper gun, R-pentomino);
+* agreement of three independent restatements: numpy twin, C stepper, C++ actor protocol
+  (GameOfLifeLogic.fs:39-71 message for message, under the Reset->State phase barrier);
+* the committed golden fixtures (tests/golden/make_golden.py).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+# ---------------------------------------------------------------- .NET System.Random
+@pytest.mark.parametrize("seed,first", [(0, 1559595546), (1, 534011718), (42, 1434747710)])
+def test_dotnet_random_published_values(oracle, seed, first):
+    assert oracle.DotNetRandom(seed).next() == first
+
+
+def test_dotnet_random_python_matches_c(oracle):
+    import ctypes
+
+    lib = oracle.c_oracle()
+    for seed in (0, 1, 42, -7, 2**31 - 1, -(2**31), 161803398, 123456789):
+        buf = ctypes.create_string_buffer(64 * 4 + 16)
+        lib.dn_random_init(buf, seed)
+        r = oracle.DotNetRandom(seed)
+        for i in range(300):
+            if i % 3 == 2:
+                assert r.next(2) == lib.dn_random_next_max(buf, 2)
+            else:
+                assert r.next() == lib.dn_random_next(buf)
+
+
+def test_seed_modes_match_c(oracle):
+    for mode in (0, 1):
+        for w, h, seed in ((100, 100, 42), (37, 5, -3), (3, 64, 9)):
+            assert np.array_equal(oracle.seed_dotnet(w, h, seed, mode), oracle.c_seed_dotnet(w, h, seed, mode))
+    assert np.array_equal(oracle.seed_splitmix(200, 17, 0x5EED), oracle.c_seed_splitmix(200, 17, 0x5EED))
+
+
+def test_seed_dotnet_order_is_x_major(oracle):
+    # GameOfLifeDriver.fs:16-19: RNG call k -> cell (x = k / H, y = k % H)
+    w, h = 7, 5
+    r = oracle.DotNetRandom(11)
+    draws = [r.next() % 2 == 0 for _ in range(w * h)]
+    b = oracle.seed_dotnet(w, h, 11, 0)
+    for k, alive in enumerate(draws):
+        assert b[k % h, k // h] == alive
+
+
+# ---------------------------------------------------------------- stepper agreement
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_numpy_twin_matches_c_stepper(oracle, boundary):
+    rng = np.random.default_rng(1)
+    for w, h in ((3, 3), (4, 7), (33, 19), (64, 64), (101, 3)):
+        b = (rng.random((h, w)) < 0.4).astype(np.uint8)
+        assert np.array_equal(oracle.run(b, 25, boundary), oracle.c_run(b, 25, boundary))
+
+
+def test_hash_twin_matches_c(oracle):
+    rng = np.random.default_rng(2)
+    for w, h in ((3, 3), (64, 2), (65, 9), (128, 31), (1000, 3)):
+        b = (rng.random((h, w)) < 0.5).astype(np.uint8)
+        assert oracle.board_hash(b) == oracle.c_hash(b)
+
+
+def test_small_boards_rejected(oracle):
+    with pytest.raises(ValueError):
+        oracle.step(np.zeros((2, 5), np.uint8))
+
+
+# ---------------------------------------------------------------- known answers (external pins)
+def test_blinker_period_two(oracle):
+    for bd in (0, 1):
+        b = np.zeros((8, 8), np.uint8)
+        oracle.place_rle(b, oracle.BLINKER, 2, 3)
+        b1 = oracle.step(b, bd)
+        assert not np.array_equal(b1, b) and np.array_equal(oracle.step(b1, bd), b)
+
+
+def test_block_still_life(oracle):
+    b = np.zeros((6, 6), np.uint8)
+    oracle.place_rle(b, oracle.BLOCK, 2, 2)
+    assert np.array_equal(oracle.step(b, 0), b)
+
+
+def test_full_torus_dies(oracle):
+    assert oracle.population(oracle.step(np.ones((8, 8), np.uint8), 0)) == 0
+
+
+def test_glider_returns_after_4w_on_torus(oracle):
+    b = np.zeros((32, 32), np.uint8)
+    oracle.place_rle(b, oracle.GLIDER, 5, 9)
+    assert np.array_equal(oracle.c_run(b, 128, 0), b)
+    assert not np.array_equal(oracle.c_run(b, 64, 0), b)
+
+
+def test_gosper_gun(oracle):
+    b = np.zeros((64, 64), np.uint8)
+    oracle.place_rle(b, oracle.GOSPER_GUN, 1, 1)
+    assert oracle.population(b) == 36
+    assert oracle.population(oracle.run(b, 30, 1)) == 41  # gun + 1 glider
+
+
+def test_r_pentomino_stabilises_at_116(oracle):
+    # 768^2 torus: debris and the six escaping gliders stay clear of the wrap for 1103 generations
+    b = np.zeros((768, 768), np.uint8)
+    oracle.place_rle(b, oracle.R_PENTOMINO, 383, 383)
+    assert oracle.population(oracle.c_run(b, 1103, 0)) == 116
+
+
+# ---------------------------------------------------------------- actor protocol restatement
+def _actor(w, h, gens, threads, seed, init="dotnet-mod2"):
+    exe = os.path.join(ROOT, "oracle", "build", "actor_protocol")
+    out = subprocess.run([exe, str(w), str(h), str(gens), str(threads), str(seed), "0", init],
+                         check=True, capture_output=True, text=True).stdout
+    return json.loads(out)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42])
+def test_actor_protocol_equals_synchronous_oracle_c1(oracle, seed):
+    # the reference's default board (100x100 torus), dotnet-mod2 init, 100 generations
+    r = _actor(100, 100, 100, 4, seed)
+    b = oracle.c_run(oracle.seed_dotnet(100, 100, seed, 0), 100, 0)
+    assert r["hash"] == oracle.c_hash(b)
+    assert r["population"] == oracle.population(b)
+    assert r["messages"] == 100 * (18 * 100 * 100 + 1)  # 18 messages per cell per generation + view reset
+
+
+def test_actor_protocol_ragged_board(oracle):
+    r = _actor(37, 23, 40, 8, 0x5EED, "splitmix")
+    b = oracle.c_run(oracle.seed_splitmix(37, 23, 0x5EED), 40, 0)
+    assert r["hash"] == oracle.c_hash(b)
+
+
+# ---------------------------------------------------------------- golden fixtures
+def _golden():
+    with open(os.path.join(HERE, "golden", "golden_small.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _initial(oracle, case):
+    w, h = case["width"], case["height"]
+    if case["init"] == "dotnet-mod2":
+        return oracle.seed_dotnet(w, h, case["seed"], 0)
+    if case["init"] == "dotnet-next2":
+        return oracle.seed_dotnet(w, h, case["seed"], 1)
+    if case["init"] == "splitmix":
+        return oracle.seed_splitmix(w, h, case["seed"])
+    b = np.zeros((h, w), np.uint8)
+    pats = {"gosper_gun": oracle.GOSPER_GUN, "r_pentomino": oracle.R_PENTOMINO}
+    for name, x, y in case["rle"]:
+        oracle.place_rle(b, pats[name], x, y)
+    return b
+
+
+@pytest.mark.parametrize("name", sorted(_golden()))
+def test_oracle_reproduces_golden(oracle, name):
+    case = _golden()[name]
+    bd = 0 if case["boundary"] == "torus" else 1
+    b = _initial(oracle, case)
+    done = 0
+    for cp in sorted(int(c) for c in case["checkpoints"]):
+        b = oracle.c_run(b, cp - done, bd)
+        done = cp
+        want = case["checkpoints"][str(cp)]
+        assert str(oracle.c_hash(b)) == want["hash"] and oracle.population(b) == want["population"]
+
+
+def test_render_gray8_layout(oracle):
+    b = np.zeros((3, 4), np.uint8)
+    b[1, 2] = 1  # cell (x=2, y=1)
+    px = oracle.render_gray8(b, 128, stride=6)
+    assert px.shape == (18,) and px[2 + 1 * 6] == 128 and px.sum() == 128
+
+
+def test_rle_parser(oracle):
+    assert sorted(oracle.parse_rle("#C comment\nx = 3, y = 3, rule = B3/S23\nbo$2bo$3o!")) == sorted(
+        [(1, 0), (2, 1), (0, 2), (1, 2), (2, 2)]
+    )
+    assert len(oracle.parse_rle(oracle.GOSPER_GUN)) == 36

@@ -1,0 +1,48 @@
+"""Sweep temporal-block depth k (and optionally segment rows) on one GPU; prints one JSON line per config.
+
+    python tools/sweep.py --size 65536 --ks 1,2,4,8,16,24,32 --passes 8
+Timing: HIP events on the board's own stream around `passes` launches (after 2 warm-up launches).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--size", type=int, default=65536)
+    p.add_argument("--height", type=int, default=0)
+    p.add_argument("--ks", default="1,2,4,8,16,24,32")
+    p.add_argument("--passes", type=int, default=8)
+    p.add_argument("--boundary", type=int, default=0)
+    a = p.parse_args()
+    import torch
+
+    from gameoflifewithactors_amd import Board
+
+    W = a.size
+    H = a.height or a.size
+    for k in [int(x) for x in a.ks.split(",")]:
+        with Board(W, H, a.boundary, tblock_k=k) as b:
+            b.seed_splitmix(0x5EED)
+            s = torch.cuda.ExternalStream(b.stream)
+            b.step(2 * k)
+            b.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            b.step(a.passes * k)
+            e1.record(s)
+            b.synchronize()
+            t = e0.elapsed_time(e1) / 1e3 / a.passes
+            gcups = W * H * k / t / 1e9
+            print(json.dumps({"W": W, "H": H, "k": k, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
+                              "alg_GBps": round(W * H / 4 / t / 1e9, 1),
+                              "valu_Tops": round(13 * W * H / 32 * k / t / 1e12, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
