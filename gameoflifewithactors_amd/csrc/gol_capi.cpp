@@ -130,20 +130,6 @@ __global__ void set_points_bytes(uint8_t* cells, int64_t W, const int64_t* xy, i
     cells[xy[2 * i] + xy[2 * i + 1] * W] = 1;
 }
 
-int64_t pick_seg(int64_t out_rows, int64_t nstrips, int k) {
-    static const int64_t env_seg = [] {
-        const char* s = std::getenv("GOL_SEG_ROWS");
-        return s ? std::atoll(s) : 0LL;
-    }();
-    static const int64_t target_waves = [] {
-        const char* s = std::getenv("GOL_TARGET_WAVES");
-        return s ? std::atoll(s) : 4096LL;
-    }();
-    int64_t seg = env_seg > 0 ? env_seg : (out_rows * nstrips + target_waves - 1) / std::max<int64_t>(1, target_waves);
-    seg = std::max<int64_t>(seg, std::max<int64_t>(8 * (int64_t)k, 64));
-    return std::min<int64_t>(std::max<int64_t>(seg, 1), std::max<int64_t>(out_rows, 1));
-}
-
 bool valid_k(int k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 24 || k == 32; }
 
 int largest_k_at_most(int64_t n, int cap) {
@@ -183,7 +169,7 @@ struct gol_board {
         a.height = H;
         a.out_begin = out_begin;
         a.out_end = out_end;
-        a.seg = pick_seg(out_end - out_begin, gol::stream_strips(a.words), k);
+        a.seg = 0;
         return a;
     }
 };
@@ -571,10 +557,14 @@ int gol_stream(gol_board* b, void** stream) {
 int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows) {
     if (int rc = check_strip(s)) return rc;
     if (!valid_k(k)) return fail(GOL_ERR_INVALID, "k must be one of 1,2,4,8,16,24,32");
-    const int64_t nstrips = gol::stream_strips(s->width / 32);
-    const int64_t seg = pick_seg(out_end - out_begin, nstrips, k);
-    if (seg_rows) *seg_rows = seg;
-    if (waves) *waves = nstrips * ((out_end - out_begin + seg - 1) / seg);
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    gol::StreamArgs a{};
+    a.words = s->width / 32;
+    a.out_begin = out_begin;
+    a.out_end = out_end;
+    gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
+    if (seg_rows) *seg_rows = a.seg;
+    if (waves) *waves = a.nstrips * a.nsegs;
     return GOL_OK;
 }
 
@@ -604,7 +594,7 @@ int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k
     a.height = s->height;
     a.out_begin = out_begin;
     a.out_end = out_end;
-    a.seg = pick_seg(out_end - out_begin, gol::stream_strips(a.words), k);
+    a.seg = 0;
     GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0,
                                     (hipStream_t)stream));
     return GOL_OK;

@@ -15,12 +15,14 @@ struct StreamArgs {
     int64_t height;     // global board height
     int64_t out_begin;  // owned rows [out_begin, out_end) are produced
     int64_t out_end;
-    int64_t seg;        // rows per wave segment
+    int64_t seg;        // rows per wave segment (plan_stream)
     int64_t nstrips;    // filled by the launcher
     int64_t nsegs;      // filled by the launcher
 };
 
 int64_t stream_strips(int64_t words);
+// fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
+void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s);
 hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s);

@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <cstdlib>
+
 #include "gol_bitlogic.h"
 #include "gol_internal.h"
 
@@ -379,10 +382,89 @@ static hipError_t launch_stream_k(const uint32_t* src, uint32_t* dst, const Stre
 
 int64_t stream_strips(int64_t words) { return (words + kInterior - 1) / kInterior; }
 
+template <int K>
+static const void* stream_kernel(bool bounded, bool wrap) {
+    if (bounded) return wrap ? (const void*)&gol_stream_step<K, true, true> : (const void*)&gol_stream_step<K, true, false>;
+    return wrap ? (const void*)&gol_stream_step<K, false, true> : (const void*)&gol_stream_step<K, false, false>;
+}
+
+static int k_index(int k) {
+    switch (k) {
+        case 1: return 0;
+        case 2: return 1;
+        case 4: return 2;
+        case 8: return 3;
+        case 16: return 4;
+        case 24: return 5;
+        case 32: return 6;
+        default: return -1;
+    }
+}
+
+// Waves of gol_stream_step<K> the current device holds at once (occupancy x CUs), cached per variant.
+// Falls back to 4096 when no device answers (host-only planning, e.g. CPU tests).
+static int64_t resident_waves(int k, bool bounded, bool wrap) {
+    static std::atomic<int64_t> cache[7][2][2];
+    const int ki = k_index(k);
+    if (ki < 0) return 4096;
+    int64_t v = cache[ki][bounded][wrap].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    const void* fn = nullptr;
+    switch (k) {
+        case 1: fn = stream_kernel<1>(bounded, wrap); break;
+        case 2: fn = stream_kernel<2>(bounded, wrap); break;
+        case 4: fn = stream_kernel<4>(bounded, wrap); break;
+        case 8: fn = stream_kernel<8>(bounded, wrap); break;
+        case 16: fn = stream_kernel<16>(bounded, wrap); break;
+        case 24: fn = stream_kernel<24>(bounded, wrap); break;
+        case 32: fn = stream_kernel<32>(bounded, wrap); break;
+    }
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kWave * kWavesPerBlock, 0) != hipSuccess ||
+        blocks <= 0 || cus <= 0) {
+        (void)hipGetLastError();
+        return 4096;
+    }
+    v = (int64_t)blocks * cus * kWavesPerBlock;
+    cache[ki][bounded][wrap].store(v, std::memory_order_relaxed);
+    return v;
+}
+
+// Work decomposition: nstrips column strips x nsegs row segments, one wave each.  The segment count
+// is chosen so the grid is ONE balanced round of resident waves (a partial second round would leave a
+// tail of lone waves), with segments no shorter than 2K rows (pipeline fill cost).  GOL_SEG_ROWS
+// overrides the segment length (experiments).
+void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
+    static const int64_t env_seg = [] {
+        const char* e = std::getenv("GOL_SEG_ROWS");
+        return e ? std::atoll(e) : 0LL;
+    }();
+    a.nstrips = stream_strips(a.words);
+    const int64_t rows = a.out_end - a.out_begin;
+    if (rows <= 0) {
+        a.nsegs = 0;
+        a.seg = 1;
+        return;
+    }
+    int64_t seg = env_seg;
+    if (seg <= 0) {
+        const int64_t slots = resident_waves(k, bounded, wrap);
+        int64_t nsegs = slots / a.nstrips;
+        if (nsegs < 1) nsegs = 1;
+        const int64_t min_seg = 2 * k > 16 ? 2 * k : 16;
+        const int64_t max_segs = rows / min_seg > 0 ? rows / min_seg : 1;
+        if (nsegs > max_segs) nsegs = max_segs;
+        seg = (rows + nsegs - 1) / nsegs;
+    }
+    a.seg = seg;
+    a.nsegs = (rows + seg - 1) / seg;
+}
+
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s) {
-    a.nstrips = stream_strips(a.words);
-    a.nsegs = (a.out_end - a.out_begin + a.seg - 1) / a.seg;
+    plan_stream(a, k, bounded, wrap);
     if (a.nsegs <= 0) return hipSuccess;
     switch (k) {
         case 1: return launch_stream_k<1>(src, dst, a, bounded, wrap, s);

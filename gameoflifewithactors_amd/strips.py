@@ -17,6 +17,10 @@ wrap-rows layout (no ghosts, one launch per pass).
 The compute itself goes through an *engine*; the product engine is `HipEngine` (the C ABI,
 gol_strip_* in include/gol/gol.h).  Tests may inject a CPU engine to exercise partitioning and the
 exchange protocol with gloo; the product path never falls back to one.
+
+The halo exchange goes through an *exchanger*: `DistExchange` (torch.distributed point-to-point, one
+process per GPU -- the bench path) or `LocalExchange` (several strips driven by one process, copied
+device-to-device; `LocalBoard` uses it to run N strips on the GPUs of one process).
 """
 from __future__ import annotations
 
@@ -108,7 +112,7 @@ class StripRunner:
     """One rank's strip of a width x height board; `k` generations per pass."""
 
     def __init__(self, width: int, height: int, boundary: int, k: int, rank: int = 0, world: int = 1,
-                 device: torch.device | None = None, engine=None, group=None):
+                 device: torch.device | None = None, engine=None, group=None, exchanger=None):
         if width % 32:
             raise ValueError("row strips need width % 32 == 0 (bit-packed layout)")
         if boundary not in (TORUS, BOUNDED):
@@ -129,6 +133,7 @@ class StripRunner:
         self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else _NullStream()
         self.up = (rank - 1) % world if (boundary == TORUS or rank > 0) else None
         self.down = (rank + 1) % world if (boundary == TORUS or rank < world - 1) else None
+        self.exchanger = exchanger if exchanger is not None else DistExchange(group)
 
     # ---------------------------------------------------------------- state
     def seed_splitmix(self, seed: int) -> None:
@@ -145,24 +150,16 @@ class StripRunner:
         return self.engine.get_cells(self.geom, self.bufs[self.cur], self.compute_stream)
 
     # ---------------------------------------------------------------- one pass
-    def _exchange(self, buf: torch.Tensor, k: int):
-        """Post the halo exchange of `k` rows; returns the request list (empty when N = 1)."""
+    def post_exchange(self, k: int | None = None):
+        """Start the halo exchange of the current buffer; returns waitables."""
+        k = self.k if k is None else k
         if self.world == 1:
             return []
-        g, h = self.geom.ghost, self.geom.rows
-        ops = []
-        if self.up is not None:  # my top rows -> up's bottom ghost; up's bottom rows -> my top ghost
-            ops.append(dist.P2POp(dist.isend, buf[g:g + k], self.up, self.group, tag=1))
-        if self.down is not None:
-            ops.append(dist.P2POp(dist.isend, buf[g + h - k:g + h], self.down, self.group, tag=2))
-        if self.down is not None:
-            ops.append(dist.P2POp(dist.irecv, buf[g + h:g + h + k], self.down, self.group, tag=1))
-        if self.up is not None:
-            ops.append(dist.P2POp(dist.irecv, buf[g - k:g], self.up, self.group, tag=2))
-        return dist.batch_isend_irecv(ops) if ops else []
+        with _stream_ctx(self.compute_stream):
+            return self.exchanger.post(self, self.bufs[self.cur], k)
 
-    def step_pass(self, k: int | None = None) -> None:
-        """Advance k (default self.k) generations: exchange || interior, then boundary rows."""
+    def compute(self, reqs, k: int | None = None) -> None:
+        """Interior rows (overlapping the exchange), wait, then the boundary rows; swap buffers."""
         k = self.k if k is None else k
         src, dst = self.bufs[self.cur], self.bufs[self.cur ^ 1]
         h = self.geom.rows
@@ -170,8 +167,6 @@ class StripRunner:
         if self.world == 1:
             self.engine.step(self.geom, src, dst, k, 0, h, s)
         else:
-            with _stream_ctx(s):
-                reqs = self._exchange(src, k)
             lo, hi = min(k, h), max(h - k, min(k, h))
             self.engine.step(self.geom, src, dst, k, lo, hi, s)  # interior overlaps the exchange
             with _stream_ctx(s):
@@ -181,6 +176,10 @@ class StripRunner:
             self.engine.step(self.geom, src, dst, k, hi, h, s)
         self.cur ^= 1
         self.generation += k
+
+    def step_pass(self, k: int | None = None) -> None:
+        """Advance k (default self.k) generations: exchange || interior, then boundary rows."""
+        self.compute(self.post_exchange(k), k)
 
     def step(self, generations: int) -> None:
         while generations > 0:
@@ -208,6 +207,104 @@ class StripRunner:
 
     def hash(self) -> int:
         return int(_lib.load().gol_hash_finalize(self._reduce("hash"), self.width, self.height))
+
+
+class DistExchange:
+    """Halo exchange with torch.distributed point-to-point ops (NCCL = RCCL over xGMI on GPUs, gloo on
+    CPU).  Every rank issues its ops in the same order, so NCCL's in-order matching per peer pairs
+    them even when up == down (two ranks on a torus); gloo matches on the tags."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def post(self, r: "StripRunner", buf: torch.Tensor, k: int):
+        g, h = r.geom.ghost, r.geom.rows
+        ops = []
+        if r.up is not None:  # my top rows -> up's bottom ghost
+            ops.append(dist.P2POp(dist.isend, buf[g:g + k], r.up, self.group, tag=1))
+        if r.down is not None:  # my bottom rows -> down's top ghost
+            ops.append(dist.P2POp(dist.isend, buf[g + h - k:g + h], r.down, self.group, tag=2))
+        if r.down is not None:
+            ops.append(dist.P2POp(dist.irecv, buf[g + h:g + h + k], r.down, self.group, tag=1))
+        if r.up is not None:
+            ops.append(dist.P2POp(dist.irecv, buf[g - k:g], r.up, self.group, tag=2))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+
+class LocalExchange:
+    """Halo exchange between strips driven by ONE process (device-to-device copies, peer copies across
+    GPUs).  All strips must post before any computes (LocalBoard does this)."""
+
+    def __init__(self):
+        self.runners: list[StripRunner] = []
+
+    def post(self, r: "StripRunner", buf: torch.Tensor, k: int):
+        g, h = r.geom.ghost, r.geom.rows
+        if r.up is not None:
+            u = self.runners[r.up]
+            ub = u.bufs[u.cur]
+            buf[g - k:g].copy_(ub[u.geom.ghost + u.geom.rows - k:u.geom.ghost + u.geom.rows], non_blocking=True)
+        if r.down is not None:
+            d = self.runners[r.down]
+            db = d.bufs[d.cur]
+            buf[g + h:g + h + k].copy_(db[d.geom.ghost:d.geom.ghost + k], non_blocking=True)
+        return []
+
+
+class LocalBoard:
+    """N row strips of one board driven by one process (strip i on devices[i % len(devices)]).
+    Used to exercise the strip kernels and ghost geometry on a single GPU, and as an in-process
+    multi-GPU mode."""
+
+    def __init__(self, width: int, height: int, boundary: int, k: int, nstrips: int, devices=None, engine_factory=None):
+        devices = devices or [torch.device("cuda", torch.cuda.current_device())]
+        self.exchange = LocalExchange()
+        self.runners = []
+        for i in range(nstrips):
+            dev = devices[i % len(devices)]
+            eng = engine_factory(dev) if engine_factory else None
+            r = StripRunner(width, height, boundary, k, rank=i, world=nstrips, device=dev, engine=eng,
+                            exchanger=self.exchange)
+            self.runners.append(r)
+        self.exchange.runners = self.runners
+        self.width, self.height, self.k = width, height, k
+
+    def _sync_all(self):
+        for r in self.runners:
+            r.compute_stream.synchronize()
+
+    def step_pass(self, k: int | None = None) -> None:
+        self._sync_all()  # every strip's current buffer is final before anyone copies from it
+        reqs = [r.post_exchange(k) for r in self.runners]
+        self._sync_all()  # ghost rows landed before anyone overwrites a neighbour's source buffer
+        for r, q in zip(self.runners, reqs):
+            r.compute(q, k)
+
+    def step(self, generations: int) -> None:
+        while generations > 0:
+            k = self.k if generations >= self.k else _largest_k(generations)
+            self.step_pass(k)
+            generations -= k
+
+    def set_cells(self, cells) -> None:
+        for r in self.runners:
+            r.set_cells(cells[r.geom.y0:r.geom.y0 + r.geom.rows])
+
+    def get_cells(self):
+        self._sync_all()
+        return torch.cat([r.get_cells() for r in self.runners], dim=0)
+
+    def seed_splitmix(self, seed: int) -> None:
+        for r in self.runners:
+            r.seed_splitmix(seed)
+
+    def hash(self) -> int:
+        total = 0
+        for r in self.runners:
+            acc = r.engine.reduce(r.geom, r.bufs[r.cur], "hash", r.compute_stream)
+            r.compute_stream.synchronize()
+            total = (total + int(acc.item())) & 0xFFFFFFFFFFFFFFFF
+        return int(_lib.load().gol_hash_finalize(total, self.width, self.height))
 
 
 def _largest_k(n: int) -> int:
