@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgol_hip.so")
+LIB_PATH = os.environ.get("GOL_LIB") or os.path.join(HERE, "libgol_hip.so")  # GOL_LIB: A/B experiments only
 
 GOL_OK = 0
 GOL_ERR_INVALID = -1

@@ -36,13 +36,15 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tuple = ()) -> str:
+    """Compile SOURCES for gfx950 into `lib`.  `defines` (e.g. ("GOL_XLANE=0",)) build A/B variants."""
     deps = SOURCES + HEADERS + [os.path.abspath(__file__)]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if not force and not _stale(lib, deps):
+        return lib
     objs = []
+    tag = "_".join(d.replace("=", "") for d in defines)
     for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = os.path.join(CSRC, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")
         cmd = [
             _hipcc(),
             f"--offload-arch={ARCH}",
@@ -58,16 +60,16 @@ def build(force: bool = False, verbose: bool = True) -> str:
             src,
             "-o",
             obj,
-        ]
+        ] + [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

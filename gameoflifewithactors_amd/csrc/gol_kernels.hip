@@ -31,12 +31,34 @@ static constexpr int kWave = 64;
 static constexpr int kInterior = kWave - 2;  // words stored per wave column strip
 static constexpr int kWavesPerBlock = 4;
 
-__device__ __forceinline__ uint32_t dpp_from_left(uint32_t v) {  // lane i <- lane i-1 (wave_shr:1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
-}
-__device__ __forceinline__ uint32_t dpp_from_right(uint32_t v) {  // lane i <- lane i+1 (wave_shl:1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
-}
+// Cross-lane word exchange.  GOL_XLANE selects the mechanism (measured in tools/ubench/valu_rates.hip:
+// a DPP move costs a half-rate VALU issue slot pair on gfx950; ds_bpermute_b32 runs on the LDS pipe
+// and leaves the VALU free):
+//   0 = DPP wave_shr:1 / wave_shl:1 (both directions on the VALU)
+//   1 = ds_bpermute_b32 for both directions (LDS crossbar)
+//   2 = left via DPP, right via ds_bpermute (split the two pipes)
+#ifndef GOL_XLANE
+#define GOL_XLANE 2
+#endif
+struct XLane {
+    int left_addr, right_addr;  // byte addresses of lane-1 / lane+1 for ds_bpermute
+    __device__ __forceinline__ explicit XLane(int lane)
+        : left_addr(((lane - 1) & 63) << 2), right_addr(((lane + 1) & 63) << 2) {}
+    __device__ __forceinline__ uint32_t from_left(uint32_t v) const {  // lane i <- lane i-1
+#if GOL_XLANE == 1
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(left_addr, (int)v);
+#else
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);  // wave_shr:1
+#endif
+    }
+    __device__ __forceinline__ uint32_t from_right(uint32_t v) const {  // lane i <- lane i+1
+#if GOL_XLANE == 0
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
+#else
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(right_addr, (int)v);
+#endif
+    }
+};
 
 __device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t m) {
     int64_t r = a % m;
@@ -57,10 +79,10 @@ __device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t m) {
 // One level for one row: window (prev = P, cur = C) + new row v -> next generation of the C row.
 // The new row's sums overwrite the P slot (it becomes the C slot of the following row).
 template <bool MASK>
-__device__ __forceinline__ uint32_t level_row(uint32_t v, uint32_t& sP, uint32_t& cP, uint32_t sC, uint32_t cC,
-                                              uint32_t alC, uint32_t rowmask) {
+__device__ __forceinline__ uint32_t level_row(const XLane& xl, uint32_t v, uint32_t& sP, uint32_t& cP, uint32_t sC,
+                                              uint32_t cC, uint32_t alC, uint32_t rowmask) {
     uint32_t sN, cN;
-    row_sum(dpp_from_left(v), v, dpp_from_right(v), sN, cN);
+    row_sum(xl.from_left(v), v, xl.from_right(v), sN, cN);
     uint32_t out = life_next(sP, cP, sC, cC, sN, cN, alC);
     sP = sN;
     cP = cN;
@@ -72,85 +94,81 @@ __device__ __forceinline__ uint32_t level_row(uint32_t v, uint32_t& sP, uint32_t
 // fewer for the VALU-bound deep passes (registers go to the K level windows instead).
 template <int K>
 struct TripRows {
-    static constexpr int value = K == 1 ? 8 : (K <= 4 ? 4 : 4);
+    static constexpr int value = K == 1 ? 8 : 4;
 };
 
+// One wavefront's pipeline: K generation levels of 3-row windows held in registers.
 template <int K, bool BOUNDED, bool WRAP_ROWS>
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const uint32_t* __restrict__ src,
-                                                                          uint32_t* __restrict__ dst,
-                                                                          StreamArgs a) {
-    constexpr int R = TripRows<K>::value;
+struct StreamWave {
+    static constexpr int R = TripRows<K>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
-    const int lane = threadIdx.x & (kWave - 1);
-    // wave index made provably uniform so all row bookkeeping below lives in SGPRs
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    if (gw >= a.nstrips * a.nsegs) return;
-    const int64_t sx = gw % a.nstrips;
-    const int64_t sy = gw / a.nstrips;
 
-    const int64_t cw = sx * kInterior - 1 + lane;  // this lane's word column (may be off-board)
-    uint32_t lc;                                    // column actually loaded
-    uint32_t colmask = 0xffffffffu;
-    if (BOUNDED) {
-        const bool in = cw >= 0 && cw < a.words;
-        colmask = in ? 0xffffffffu : 0u;
-        lc = in ? (uint32_t)cw : 0u;
-    } else {
-        lc = (uint32_t)floor_mod(cw, a.words);
-    }
-    const bool store_lane = lane >= 1 && lane <= kInterior && cw < a.words;
+    const uint32_t* __restrict__ src;
+    uint32_t* __restrict__ dst;
+    const StreamArgs& a;
+    XLane xl;
+    uint32_t lc;       // loaded word column (per lane)
+    uint32_t colmask;  // bounded: ~0 for on-board columns
+    bool store_lane;
+    int64_t seg_begin, seg_end, nsteps, ly0;
+    int64_t load_br;  // buffer row of the next level-0 row to load (uniform)
 
-    const int64_t seg_begin = a.out_begin + sy * a.seg;
-    const int64_t seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
-    const int64_t nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
-    const int64_t ntrips = (nsteps + R - 1) / R;
-    const int64_t ly0 = seg_begin - K;                     // level-0 row of step 0
+    // level state: two row slots (X, Y) of row sums (s, c) and the raw centre word of the Y slot
+    uint32_t sX[K], cX[K], sY[K], cY[K], aY[K];
 
-    // level state: two row slots (X, Y) of row sums (s, c) and raw words (a)
-    uint32_t sX[K], cX[K], aX[K], sY[K], cY[K], aY[K];
+    __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
+                                          int64_t sx, int64_t sy)
+        : src(s), dst(d), a(args), xl(lane) {
+        const int64_t cw = sx * kInterior - 1 + lane;  // this lane's word column (may be off-board)
+        if (BOUNDED) {
+            const bool in = cw >= 0 && cw < a.words;
+            colmask = in ? 0xffffffffu : 0u;
+            lc = in ? (uint32_t)cw : 0u;
+        } else {
+            colmask = 0xffffffffu;
+            lc = (uint32_t)floor_mod(cw, a.words);
+        }
+        store_lane = lane >= 1 && lane <= kInterior && cw < a.words;
+        seg_begin = a.out_begin + sy * a.seg;
+        seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
+        nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
+        ly0 = seg_begin - K;                     // level-0 row of step 0
+        load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
 #pragma unroll
-    for (int g = 0; g < K; g++) sX[g] = cX[g] = aX[g] = sY[g] = cY[g] = aY[g] = 0;
+        for (int g = 0; g < K; g++) sX[g] = cX[g] = sY[g] = cY[g] = aY[g] = 0;
+    }
 
-    // buffer row of the first row of trip t (uniform cursor)
-    int64_t br_trip = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
-    auto load_trip = [&](int64_t t, int64_t br_first, uint32_t (&buf)[R]) {
+    // Load the next R level-0 rows.  Loads are unconditional (addresses clamped; values masked) so the
+    // number of memory operations per trip is fixed and the compiler can wait for exactly the loads.
+    __device__ __forceinline__ void load(uint32_t (&buf)[R], int64_t first_step) {
+        const int64_t buf_rows = a.rows + 2 * a.ghost;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const int64_t step = t * R + r;
-            const int64_t ly = ly0 + step;
-            bool ld = step < nsteps;
-            if (BOUNDED) ld = ld && a.y0 + ly >= 0 && a.y0 + ly < a.height;
-            int64_t brr = br_first + r;
+            int64_t br = load_br;
             if (WRAP_ROWS) {
-                if (brr >= a.rows) brr -= a.rows;
-                if (brr >= a.rows) brr %= a.rows;
+                load_br = br + 1 == a.rows ? 0 : br + 1;
+            } else {
+                load_br = br + 1;
+                br = br < buf_rows ? br : buf_rows - 1;  // past the segment's last step: value unused
             }
-            buf[r] = ld ? src[brr * a.pitch + lc] : 0u;
-            if (BOUNDED) buf[r] &= colmask;
+            uint32_t v = src[br * a.pitch + lc];
+            if (BOUNDED) {
+                const int64_t gy = a.y0 + ly0 + first_step + r;
+                v = (gy >= 0 && gy < a.height) ? (v & colmask) : 0u;
+            }
+            buf[r] = v;
         }
-    };
-    auto advance = [&](int64_t br_first) {
-        int64_t n = br_first + R;
-        if (WRAP_ROWS) {
-            if (n >= a.rows) n -= a.rows;
-            if (n >= a.rows) n %= a.rows;
-        }
-        return n;
-    };
+    }
 
-    uint32_t nxt[R];
-    load_trip(0, br_trip, nxt);
-    for (int64_t t = 0; t < ntrips; t++) {
-        uint32_t v[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) v[r] = nxt[r];
-        br_trip = advance(br_trip);
-        if (t + 1 < ntrips) load_trip(t + 1, br_trip, nxt);  // prefetch the next trip's rows
-
+    // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
+    // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
+    template <bool SKIP>
+    __device__ __forceinline__ void process(uint32_t (&v)[R], int64_t t) {
         const int64_t lyt = ly0 + t * R;
 #pragma unroll
         for (int g = 0; g < K; g++) {
+            // level g's input rows in this trip are valid only from step 2g on
+            if (SKIP && t * R + R - 1 < 2 * g) continue;
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
@@ -160,22 +178,86 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const u
                     m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
-                const uint32_t o0 = level_row<BOUNDED>(v[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0);
-                aX[g] = v[r];
-                const uint32_t o1 = level_row<BOUNDED>(v[r + 1], sY[g], cY[g], sX[g], cX[g], aX[g], m1);
+                const uint32_t o0 = level_row<BOUNDED>(xl, v[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0);
+                const uint32_t o1 = level_row<BOUNDED>(xl, v[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1);
                 aY[g] = v[r + 1];
                 v[r] = o0;
                 v[r + 1] = o1;
             }
         }
-        // v[r] is now row (lyt + r - K) of generation K
+    }
+
+    __device__ __forceinline__ void store_all(const uint32_t (&v)[R], int64_t t) {
+        const int64_t lo = ly0 + t * R - K;
         if (store_lane) {
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-                const int64_t lo = lyt + r - K;
-                if (lo >= seg_begin && lo < seg_end) dst[(WRAP_ROWS ? lo : lo + a.ghost) * a.pitch + lc] = v[r];
-            }
+            for (int r = 0; r < R; r++) dst[((WRAP_ROWS ? 0 : a.ghost) + lo + r) * a.pitch + lc] = v[r];
         }
+    }
+
+    __device__ __forceinline__ void store_masked(const uint32_t (&v)[R], int64_t t) {
+        const int64_t lo = ly0 + t * R - K;
+        if (store_lane) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (lo + r >= seg_begin && lo + r < seg_end) dst[((WRAP_ROWS ? 0 : a.ghost) + lo + r) * a.pitch + lc] = v[r];
+        }
+    }
+};
+
+// Temporal-blocked streaming step.  Each wave: strip `sx` (words [62*sx, 62*sx + 62)), output rows
+// [seg_begin, seg_end).  Trips: [0, t_fill) pipeline fill (no stores, garbage levels skipped),
+// [t_fill, t_tail) steady state (every row stored, fixed memory-op count per trip), [t_tail, ntrips)
+// masked tail.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch).
+template <int K, bool BOUNDED, bool WRAP_ROWS>
+__global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const uint32_t* __restrict__ src,
+                                                                          uint32_t* __restrict__ dst,
+                                                                          StreamArgs a) {
+    using W = StreamWave<K, BOUNDED, WRAP_ROWS>;
+    constexpr int R = W::R;
+    const int lane = threadIdx.x & (kWave - 1);
+    // wave index made provably uniform so all row bookkeeping lives in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    if (gw >= a.nstrips * a.nsegs) return;
+    W w(src, dst, a, lane, gw % a.nstrips, gw / a.nstrips);
+
+    const int64_t ntrips = (w.nsteps + R - 1) / R;
+    const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
+    const int64_t first_store_trip = (2 * K + R - 1) / R;
+    int64_t t_tail = (2 * K + (w.seg_end - w.seg_begin)) / R;  // trips entirely inside the stored range
+    if (t_tail < first_store_trip) t_tail = first_store_trip;
+    if (t_tail > ntrips) t_tail = ntrips;
+
+    uint32_t nxt[R], v[R];
+    w.load(nxt, 0);
+    int64_t t = 0;
+    for (; t < t_fill; t++) {
+#pragma unroll
+        for (int r = 0; r < R; r++) v[r] = nxt[r];
+        w.load(nxt, (t + 1) * R);
+        w.template process<true>(v, t);
+    }
+    for (; t < first_store_trip && t < ntrips; t++) {  // transition trip (when R does not divide 2K)
+#pragma unroll
+        for (int r = 0; r < R; r++) v[r] = nxt[r];
+        w.load(nxt, (t + 1) * R);
+        w.template process<true>(v, t);
+        w.store_masked(v, t);
+    }
+    for (; t < t_tail; t++) {  // steady state
+#pragma unroll
+        for (int r = 0; r < R; r++) v[r] = nxt[r];
+        w.load(nxt, (t + 1) * R);
+        w.template process<false>(v, t);
+        w.store_all(v, t);
+    }
+    for (; t < ntrips; t++) {  // masked tail
+#pragma unroll
+        for (int r = 0; r < R; r++) v[r] = nxt[r];
+        w.load(nxt, (t + 1) * R);
+        w.template process<false>(v, t);
+        w.store_masked(v, t);
     }
 }
 
