@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--width", type=int, default=65536)
     p.add_argument("--height", type=int, default=65536, help="rows per GPU (board height = height * gpus)")
-    p.add_argument("--tblock", type=int, default=16, help="generations per pass (1,2,4,8,16,24,32)")
+    p.add_argument("--tblock", type=int, default=0,
+                   help="generations per pass (0 = the engine's default for the board layout)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU actor baseline sample length")
@@ -104,9 +105,13 @@ def main():
     from gameoflifewithactors_amd import TORUS, BOUNDED
     from gameoflifewithactors_amd.strips import StripRunner
 
+    from gameoflifewithactors_amd import _lib
+
     boundary = TORUS if args.boundary == "torus" else BOUNDED
     W, H = args.width, args.height * world
-    k = args.tblock
+    lib = _lib.load()
+    ilv = lib.gol_default_ilv(W)
+    k = args.tblock or lib.gol_default_tblock(ilv)
     runner = StripRunner(W, H, boundary, k, rank=rank, world=world, device=torch.device("cuda", local))
     runner.seed_splitmix(args.seed)
 
@@ -168,6 +173,7 @@ def main():
                 "width": W,
                 "height": H,
                 "generations_per_step": k,
+                "interleave": ilv,
                 "boundary": args.boundary,
                 "seed": args.seed,
                 "parallelism": f"row strips x{world}" + (" (RCCL halo exchange)" if world > 1 else ""),
@@ -179,7 +185,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"gol_stream_step<K={k}>",
+                "kernel": f"gol_stream_step<K={k}, M={ilv}>",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
             },

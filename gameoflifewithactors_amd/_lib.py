@@ -48,6 +48,8 @@ class Strip(ctypes.Structure):
         ("pitch", ctypes.c_int64),
         ("boundary", ctypes.c_int32),
         ("wrap_rows", ctypes.c_int32),
+        ("ilv", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -81,6 +83,10 @@ SIGNATURES = {
     "gol_hash": (ctypes.c_int, [vp, u64p]),
     "gol_info": (ctypes.c_int, [vp, i64p, i64p, ip, ip, ip]),
     "gol_stream": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    "gol_layout": (ctypes.c_int, [vp, ip, i64p]),
+    "gol_default_ilv": (ctypes.c_int, [i64]),
+    "gol_default_tblock": (ctypes.c_int, [ctypes.c_int]),
+    "gol_supported_k": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "gol_last_error": (ctypes.c_char_p, []),
     "gol_version": (ctypes.c_char_p, []),
     "gol_strip_step": (ctypes.c_int, [sp, vp, vp, ctypes.c_int, i64, i64, vp]),

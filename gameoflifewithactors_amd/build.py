@@ -13,9 +13,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgol_hip.so")
-SOURCES = [os.path.join(CSRC, "gol_kernels.hip"), os.path.join(CSRC, "gol_capi.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gol_step.hip", "gol_formats.hip", "gol_capi.cpp")]
 HEADERS = [
     os.path.join(CSRC, "gol_bitlogic.h"),
+    os.path.join(CSRC, "gol_layout.h"),
     os.path.join(CSRC, "gol_internal.h"),
     os.path.join(ROOT, "include", "gol", "gol.h"),
 ]
@@ -43,7 +44,8 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tu
         return lib
     objs = []
     tag = "_".join(d.replace("=", "") for d in defines)
-    for src in SOURCES:
+    procs = []
+    for src in SOURCES:  # compile the translation units in parallel (gol_step.hip dominates)
         obj = os.path.join(CSRC, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")
         cmd = [
             _hipcc(),
@@ -63,8 +65,11 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tu
         ] + [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
     if verbose:
         print(" ".join(cmd), flush=True)

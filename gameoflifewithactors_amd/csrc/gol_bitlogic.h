@@ -55,6 +55,24 @@ GOL_HD void row_sum(uint32_t prev, uint32_t cur, uint32_t next, uint32_t& s, uin
     c = lut3<0xE8>(w, cur, e);
 }
 
+// Horizontal 3-sums of one block of M interleaved words (gol_layout.h: word j bit b = cell j + M*b).
+// West of word j is word j-1 at the same bit, except word 0 whose west is word M-1 one bit lower (the
+// bit below bit 0 comes from the previous block's word M-1, `prev_last`); symmetrically for east.
+// So a block costs 2 funnel shifts whatever M is (M = 1 reduces to row_sum above).
+template <int M>
+GOL_HD void row_sum_block(const uint32_t (&r)[M], uint32_t prev_last, uint32_t next_first, uint32_t (&s)[M],
+                          uint32_t (&c)[M]) {
+    const uint32_t w0 = align_right(r[M - 1], prev_last, 31);
+    const uint32_t eN = align_right(next_first, r[0], 1);
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const uint32_t w = j == 0 ? w0 : r[j - 1];
+        const uint32_t e = j == M - 1 ? eN : r[j + 1];
+        s[j] = lut3<0x96>(w, r[j], e);
+        c[j] = lut3<0xE8>(w, r[j], e);
+    }
+}
+
 // Next state of 32 cells from the three row sums (previous, centre, next row) and the centre word.
 GOL_HD uint32_t life_next(uint32_t sP, uint32_t cP, uint32_t sC, uint32_t cC, uint32_t sN, uint32_t cN,
                           uint32_t alive) {

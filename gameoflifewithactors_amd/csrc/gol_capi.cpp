@@ -117,27 +117,26 @@ bool parse_rle(const char* p, std::vector<std::pair<int64_t, int64_t>>& out, std
     return true;
 }
 
-__global__ void set_points_packed(uint32_t* words, int64_t pitch, const int64_t* xy, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t x = xy[2 * i], y = xy[2 * i + 1];
-    atomicOr(&words[y * pitch + x / 32], 1u << (x & 31));
+// temporal-block depths accepted as a cap (gol_create's tblock_k); each layout supports a subset
+bool valid_k(int k) {
+    return k == 1 || k == 2 || k == 4 || k == 6 || k == 8 || k == 12 || k == 16 || k == 24 || k == 32;
 }
 
-__global__ void set_points_bytes(uint8_t* cells, int64_t W, const int64_t* xy, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    cells[xy[2 * i] + xy[2 * i + 1] * W] = 1;
-}
-
-bool valid_k(int k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16 || k == 24 || k == 32; }
-
-int largest_k_at_most(int64_t n, int cap) {
-    static const int ks[] = {32, 24, 16, 8, 4, 2, 1};
-    for (int k : ks)
-        if (k <= cap && k <= n) return k;
+// Interleave for a packed board of this width: the widest block that divides the row (gol_layout.h).
+// GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
+int pick_ilv(int64_t width) {
+    static const int env = [] {
+        const char* e = std::getenv("GOL_ILV");
+        return e ? std::atoi(e) : 0;
+    }();
+    if ((env == 1 || env == 2 || env == 4) && width % (32 * env) == 0) return env;
+    if (width % 128 == 0) return 4;
+    if (width % 64 == 0) return 2;
     return 1;
 }
+
+// Default generations per pass for a layout (measured on MI355X, DESIGN.md "Temporal block depth").
+int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 16 : 24); }
 
 }  // namespace
 
@@ -149,6 +148,7 @@ struct gol_board {
     int boundary = GOL_TORUS;
     int tblock = 16;
     bool packed = false;
+    int ilv = 0;        // words per interleaved block (packed boards), 0 = byte board
     int64_t pitch = 0;  // words per row (packed)
     void* buf[2] = {nullptr, nullptr};
     int cur = 0;
@@ -170,6 +170,7 @@ struct gol_board {
         a.out_begin = out_begin;
         a.out_end = out_end;
         a.seg = 0;
+        a.ilv = ilv;
         return a;
     }
 };
@@ -201,7 +202,7 @@ int set_cells_impl(gol_board* b, const uint8_t* host) {
     do {
         e = hipMemcpyAsync(staging, host, n, hipMemcpyHostToDevice, b->stream);
         if (e != hipSuccess) break;
-        e = gol::launch_pack(staging, b->words(b->cur), b->W, b->H, b->pitch, 0, b->stream);
+        e = gol::launch_pack(staging, b->words(b->cur), b->W, b->H, b->pitch, 0, b->ilv, b->stream);
         if (e != hipSuccess) break;
         e = hipStreamSynchronize(b->stream);
     } while (0);
@@ -222,7 +223,8 @@ int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
             if (e != hipSuccess) break;
         }
         if (b->packed)
-            e = gol::launch_unpack(b->words(b->cur), staging, b->W, b->H, b->pitch, 0, stride, value, b->stream);
+            e = gol::launch_unpack(b->words(b->cur), staging, b->W, b->H, b->pitch, 0, stride, value, b->ilv,
+                                   b->stream);
         else
             e = gol::launch_bytes_render(b->cells(b->cur), staging, b->W, b->H, stride, value, b->stream);
         if (e != hipSuccess) break;
@@ -239,7 +241,7 @@ int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
     GOL_HIP(hipMemsetAsync(b->acc, 0, sizeof(unsigned long long), b->stream));
     if (b->packed) {
         if (hash)
-            GOL_HIP(gol::launch_hash_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, b->acc, b->stream));
+            GOL_HIP(gol::launch_hash_packed(b->words(b->cur), b->W, b->H, b->pitch, 0, 0, b->ilv, b->acc, b->stream));
         else
             GOL_HIP(gol::launch_popcount_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, b->acc, b->stream));
     } else {
@@ -266,7 +268,7 @@ int step_impl(gol_board* b, int64_t gens) {
         return GOL_OK;
     }
     while (gens > 0) {
-        const int k = largest_k_at_most(gens, b->tblock);
+        const int k = gol::stream_largest_k(gens, b->tblock, b->ilv);
         gol::StreamArgs a = b->stream_args(0, b->H, k);
         GOL_HIP(gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, k, b->boundary == GOL_BOUNDED,
                                         b->boundary == GOL_TORUS, b->stream));
@@ -287,12 +289,7 @@ int place_points(gol_board* b, const std::vector<int64_t>& xy) {
     do {
         e = hipMemcpyAsync(d, xy.data(), xy.size() * sizeof(int64_t), hipMemcpyHostToDevice, b->stream);
         if (e != hipSuccess) break;
-        const unsigned grid = (unsigned)((n + 255) / 256);
-        if (b->packed)
-            hipLaunchKernelGGL(set_points_packed, dim3(grid), dim3(256), 0, b->stream, b->words(b->cur), b->pitch, d, n);
-        else
-            hipLaunchKernelGGL(set_points_bytes, dim3(grid), dim3(256), 0, b->stream, b->cells(b->cur), b->W, d, n);
-        e = hipGetLastError();
+        e = gol::launch_set_points(b->buf[b->cur], b->packed ? b->ilv : 0, b->W, b->pitch, d, n, b->stream);
         if (e != hipSuccess) break;
         e = hipStreamSynchronize(b->stream);
     } while (0);
@@ -317,6 +314,9 @@ int check_strip(const gol_strip* s) {
     if (s->pitch < s->width / 32) return fail(GOL_ERR_INVALID, "strip pitch smaller than the row");
     if (s->ghost < 0) return fail(GOL_ERR_INVALID, "negative ghost");
     if (s->boundary != GOL_TORUS && s->boundary != GOL_BOUNDED) return fail(GOL_ERR_INVALID, "bad boundary");
+    if (s->ilv != 1 && s->ilv != 2 && s->ilv != 4) return fail(GOL_ERR_INVALID, "ilv must be 1, 2 or 4");
+    if (s->width % (32 * s->ilv) || s->pitch % s->ilv)
+        return fail(GOL_ERR_INVALID, "width must be a multiple of 32*ilv and pitch a multiple of ilv");
     if (s->wrap_rows && (s->ghost != 0 || s->rows != s->height || s->y0 != 0))
         return fail(GOL_ERR_INVALID, "wrap_rows requires the whole board in one strip with ghost = 0");
     return GOL_OK;
@@ -353,8 +353,8 @@ int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tb
         if (boundary != GOL_TORUS && boundary != GOL_BOUNDED) return fail(GOL_ERR_INVALID, "bad boundary");
         if (num_gpus != 1)
             return fail(GOL_ERR_UNSUPPORTED, "num_gpus must be 1; multi-GPU runs use one process per GPU (gol_strip_*)");
-        if (tblock_k == 0) tblock_k = 16;
-        if (!valid_k(tblock_k)) return fail(GOL_ERR_INVALID, "tblock_k must be one of 1,2,4,8,16,24,32");
+        if (tblock_k != 0 && !valid_k(tblock_k))
+            return fail(GOL_ERR_INVALID, "tblock_k must be 0 (default) or one of 1,2,4,6,8,12,16,24,32");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(GOL_ERR_NO_DEVICE, "no HIP device");
         gol_board* b = new gol_board();
@@ -363,6 +363,8 @@ int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tb
         b->boundary = boundary;
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
+        b->ilv = b->packed ? pick_ilv(width) : 0;
+        b->tblock = tblock_k ? tblock_k : default_tblock(b->ilv);
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = hipGetDevice(&b->device);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
@@ -426,7 +428,7 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
     hipError_t e = hipMalloc(&staging, (size_t)(w * h));
     if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc region");
     do {
-        e = gol::launch_region(b->buf[b->cur], b->packed, b->W, b->pitch, x, y, w, h, staging, b->stream);
+        e = gol::launch_region(b->buf[b->cur], b->packed ? b->ilv : 0, b->W, b->pitch, x, y, w, h, staging, b->stream);
         if (e != hipSuccess) break;
         e = hipMemcpyAsync(out, staging, (size_t)(w * h), hipMemcpyDeviceToHost, b->stream);
         if (e != hipSuccess) break;
@@ -466,7 +468,8 @@ int gol_seed_splitmix(gol_board* b, uint64_t seed) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
     if (b->packed)
-        GOL_HIP(gol::launch_splitmix_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, seed, b->stream));
+        GOL_HIP(gol::launch_splitmix_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, seed, b->ilv,
+                                            b->stream));
     else
         GOL_HIP(gol::launch_splitmix_bytes(b->cells(b->cur), b->W, b->H, seed, b->stream));
     b->generation = 0;
@@ -547,6 +550,25 @@ int gol_info(gol_board* b, int64_t* width, int64_t* height, int* boundary, int* 
     return GOL_OK;
 }
 
+int gol_layout(gol_board* b, int* ilv, int64_t* pitch) {
+    if (!b) return fail(GOL_ERR_INVALID, "null board");
+    if (ilv) *ilv = b->ilv;
+    if (pitch) *pitch = b->pitch;
+    return GOL_OK;
+}
+
+int gol_default_ilv(int64_t width) {
+    if (width < 32 || width % 32) return 0;
+    return pick_ilv(width);
+}
+
+int gol_default_tblock(int ilv) {
+    if (ilv != 1 && ilv != 2 && ilv != 4) return 0;
+    return default_tblock(ilv);
+}
+
+int gol_supported_k(int k, int ilv) { return gol::stream_supported(k, ilv) ? 1 : 0; }
+
 int gol_stream(gol_board* b, void** stream) {
     if (!b || !stream) return fail(GOL_ERR_INVALID, "null argument");
     *stream = (void*)b->stream;
@@ -556,12 +578,13 @@ int gol_stream(gol_board* b, void** stream) {
 // ---------------------------------------------------------------- row strips
 int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows) {
     if (int rc = check_strip(s)) return rc;
-    if (!valid_k(k)) return fail(GOL_ERR_INVALID, "k must be one of 1,2,4,8,16,24,32");
+    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a{};
     a.words = s->width / 32;
     a.out_begin = out_begin;
     a.out_end = out_end;
+    a.ilv = s->ilv;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
     if (waves) *waves = a.nstrips * a.nsegs;
@@ -572,7 +595,7 @@ int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k
                    int64_t out_end, void* stream) {
     if (int rc = check_strip(s)) return rc;
     if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
-    if (!valid_k(k)) return fail(GOL_ERR_INVALID, "k must be one of 1,2,4,8,16,24,32");
+    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     if (out_begin == out_end) return GOL_OK;
     if (!s->wrap_rows) {
@@ -595,6 +618,7 @@ int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k
     a.out_begin = out_begin;
     a.out_end = out_end;
     a.seg = 0;
+    a.ilv = s->ilv;
     GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0,
                                     (hipStream_t)stream));
     return GOL_OK;
@@ -603,7 +627,7 @@ int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k
 int gol_strip_seed_splitmix(const gol_strip* s, uint32_t* buf, uint64_t seed, void* stream) {
     if (int rc = check_strip(s)) return rc;
     if (!buf) return fail(GOL_ERR_INVALID, "null buffer");
-    GOL_HIP(gol::launch_splitmix_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost, s->y0, seed,
+    GOL_HIP(gol::launch_splitmix_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost, s->y0, seed, s->ilv,
                                         (hipStream_t)stream));
     return GOL_OK;
 }
@@ -611,7 +635,7 @@ int gol_strip_seed_splitmix(const gol_strip* s, uint32_t* buf, uint64_t seed, vo
 int gol_strip_pack(const gol_strip* s, const uint8_t* dev_cells, uint32_t* buf, void* stream) {
     if (int rc = check_strip(s)) return rc;
     if (!dev_cells || !buf) return fail(GOL_ERR_INVALID, "null buffer");
-    GOL_HIP(gol::launch_pack(dev_cells, buf, s->width, s->rows, s->pitch, s->ghost, (hipStream_t)stream));
+    GOL_HIP(gol::launch_pack(dev_cells, buf, s->width, s->rows, s->pitch, s->ghost, s->ilv, (hipStream_t)stream));
     return GOL_OK;
 }
 
@@ -619,7 +643,7 @@ int gol_strip_unpack(const gol_strip* s, const uint32_t* buf, uint8_t* dev_cells
                      void* stream) {
     if (int rc = check_strip(s)) return rc;
     if (!dev_cells || !buf || stride < s->width) return fail(GOL_ERR_INVALID, "bad buffer or stride");
-    GOL_HIP(gol::launch_unpack(buf, dev_cells, s->width, s->rows, s->pitch, s->ghost, stride, value,
+    GOL_HIP(gol::launch_unpack(buf, dev_cells, s->width, s->rows, s->pitch, s->ghost, stride, value, s->ilv,
                                (hipStream_t)stream));
     return GOL_OK;
 }
@@ -635,7 +659,7 @@ int gol_strip_population(const gol_strip* s, const uint32_t* buf, uint64_t* dev_
 int gol_strip_hash_partial(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream) {
     if (int rc = check_strip(s)) return rc;
     if (!buf || !dev_acc) return fail(GOL_ERR_INVALID, "null buffer");
-    GOL_HIP(gol::launch_hash_packed(buf, s->width / 32, s->rows, s->pitch, s->ghost, s->y0,
+    GOL_HIP(gol::launch_hash_packed(buf, s->width, s->rows, s->pitch, s->ghost, s->y0, s->ilv,
                                     (unsigned long long*)dev_acc, (hipStream_t)stream));
     return GOL_OK;
 }

@@ -1,0 +1,309 @@
+// gol_formats.hip -- data formats either side of the hot path, and the generic byte-per-cell step.
+//
+//   bytes <-> bit-packed rows (pack / unpack; unpack with value 128 or 255 is the render agent's Gray8
+//   pixel fill, GameOfLifeUI.fs:24-28 / Script.fsx:33-35), windows, device-side splitmix init,
+//   population, the canonical board hash, point placement for RLE patterns, and the byte-per-cell step
+//   used for widths that are not a multiple of 32.  Packed layouts: gol_layout.h (interleave ilv).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gol_internal.h"
+#include "gol_layout.h"
+
+namespace gol {
+
+// ------------------------------------------------------------------------------------------------
+// Generic byte-per-cell step (any width >= 3).  Rule GameOfLifeLogic.fs:59-63, torus
+// GameOfLifeDriver.fs:21-25, bounded Script.fsx:6-13.
+template <bool BOUNDED>
+__global__ __launch_bounds__(256) void gol_bytes_step(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                       int64_t W, int64_t H) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= W * H) return;
+    const int64_t x = idx % W, y = idx / W;
+    int n = 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++) {
+            if (!dx && !dy) continue;
+            int64_t nx = x + dx, ny = y + dy;
+            if (BOUNDED) {
+                if (nx < 0 || nx >= W || ny < 0 || ny >= H) continue;
+            } else {
+                nx = nx < 0 ? nx + W : (nx >= W ? nx - W : nx);
+                ny = ny < 0 ? ny + H : (ny >= H ? ny - H : ny);
+            }
+            n += src[nx + ny * W] != 0;
+        }
+    const uint8_t alive = src[idx] != 0;
+    dst[idx] = (n == 3) | ((n == 2) & alive);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packed formats.  `pitch` = words per buffer row; owned row y lives at buffer row `row0 + y`.
+
+// bytes (cells[x + y*W], nonzero = alive) -> packed words; one thread per stored word
+__global__ void gol_pack(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words, int64_t W, int64_t rows,
+                         int64_t pitch, int64_t row0, int ilv) {
+    const int64_t wpr = W / 32;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= wpr * rows) return;
+    const int64_t w = idx % wpr, y = idx / wpr;
+    const uint8_t* p = cells + y * W;
+    uint32_t v = 0;
+    for (int b = 0; b < 32; b++) v |= (uint32_t)(p[word_bit_cell(w, b, ilv)] != 0) << b;
+    words[(row0 + y) * pitch + w] = v;
+}
+
+// packed -> bytes: out[x + y*stride] = alive ? value : 0; one thread per stored word
+__global__ void gol_unpack(const uint32_t* __restrict__ words, uint8_t* __restrict__ out, int64_t W, int64_t rows,
+                           int64_t pitch, int64_t row0, int64_t stride, uint8_t value, int ilv) {
+    const int64_t wpr = W / 32;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= wpr * rows) return;
+    const int64_t w = idx % wpr, y = idx / wpr;
+    const uint32_t v = words[(row0 + y) * pitch + w];
+    uint8_t* p = out + y * stride;
+    for (int b = 0; b < 32; b++) p[word_bit_cell(w, b, ilv)] = ((v >> b) & 1u) ? value : 0;
+}
+
+// window (x0, y0, w, h) of a packed (ilv > 0) or byte (ilv == 0) board -> bytes 0/1, out[i + j*w]
+__global__ void gol_region(const void* __restrict__ board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0,
+                           int64_t w, int64_t h, uint8_t* __restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= w * h) return;
+    const int64_t x = x0 + idx % w, y = y0 + idx / w;
+    if (ilv > 0) {
+        int64_t word;
+        int bit;
+        cell_pos(x, ilv, word, bit);
+        out[idx] = (static_cast<const uint32_t*>(board)[y * pitch + word] >> bit) & 1u;
+    } else {
+        out[idx] = static_cast<const uint8_t*>(board)[y * W + x] != 0;
+    }
+}
+
+__global__ void gol_bytes_render(const uint8_t* __restrict__ cells, uint8_t* __restrict__ out, int64_t W, int64_t H,
+                                 int64_t stride, uint8_t value) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= W * H) return;
+    const int64_t x = idx % W, y = idx / W;
+    out[x + y * stride] = cells[idx] ? value : 0;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+// alive(x, y) = bit (x & 31) of low32(splitmix64(seed ^ (gy * ceil(W/32) + x/32)))  (DESIGN.md).
+// One thread per stored word; its 32 cells come from the (<= ilv) plain words of its block.
+__global__ void gol_splitmix_packed(uint32_t* __restrict__ words, int64_t wpr, int64_t rows, int64_t pitch,
+                                    int64_t row0, int64_t gy0, uint64_t seed, int ilv) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= wpr * rows) return;
+    const int64_t w = idx % wpr, y = idx / wpr;
+    const int64_t first = (w / ilv) * ilv;  // first plain word of this block
+    uint32_t plain[4];
+    for (int i = 0; i < ilv; i++) plain[i] = (uint32_t)splitmix64(seed ^ (uint64_t)((gy0 + y) * wpr + first + i));
+    uint32_t v = 0;
+    for (int b = 0; b < 32; b++) {
+        const int64_t x = word_bit_cell(w, b, ilv) - first * 32;  // cell offset inside the block
+        v |= ((plain[x >> 5] >> (x & 31)) & 1u) << b;
+    }
+    words[(row0 + y) * pitch + w] = v;
+}
+
+__global__ void gol_splitmix_bytes(uint8_t* __restrict__ cells, int64_t W, int64_t H, uint64_t seed) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= W * H) return;
+    const int64_t x = idx % W, y = idx / W, wc = (W + 31) / 32;
+    const uint32_t bits = (uint32_t)splitmix64(seed ^ (uint64_t)(y * wc + x / 32));
+    cells[idx] = (bits >> (x & 31)) & 1u;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// population (any packed layout): adds the popcount of rows [row0, row0+rows) into *acc
+__global__ void gol_popcount_packed(const uint32_t* __restrict__ words, int64_t wpr, int64_t rows, int64_t pitch,
+                                    int64_t row0, unsigned long long* acc) {
+    uint64_t sum = 0;
+    const int64_t n = wpr * rows;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x)
+        sum += __popc(words[(row0 + idx / wpr) * pitch + idx % wpr]);
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(acc, (unsigned long long)sum);
+}
+
+__global__ void gol_popcount_bytes(const uint8_t* __restrict__ cells, int64_t n, unsigned long long* acc) {
+    uint64_t sum = 0;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x)
+        sum += cells[idx] != 0;
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(acc, (unsigned long long)sum);
+}
+
+// Canonical hash partial sum: for 64-cell chunk j of global row gy, v bit i = cell 64j + i;
+// sum += fmix64(v ^ fmix64(gy * ceil(W/64) + j + phi)).  One thread per chunk.
+__global__ void gol_hash_packed(const uint32_t* __restrict__ words, int64_t W, int64_t rows, int64_t pitch,
+                                int64_t row0, int64_t gy0, int ilv, unsigned long long* acc) {
+    const int64_t nc = (W + 63) / 64;
+    const int64_t n = nc * rows;
+    uint64_t sum = 0;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = idx % nc, y = idx / nc;
+        const uint32_t* r = words + (row0 + y) * pitch;
+        uint64_t v = 0;
+        if (ilv == 1) {
+            const uint64_t lo = r[2 * j];
+            const uint64_t hi = (2 * j + 1 < W / 32) ? r[2 * j + 1] : 0u;
+            v = lo | (hi << 32);
+        } else {
+            for (int i = 0; i < 64 && 64 * j + i < W; i++) {
+                int64_t word;
+                int bit;
+                cell_pos(64 * j + i, ilv, word, bit);
+                v |= (uint64_t)((r[word] >> bit) & 1u) << i;
+            }
+        }
+        const uint64_t key = (uint64_t)((gy0 + y) * nc + j);
+        sum += fmix64(v ^ fmix64(key + 0x9E3779B97F4A7C15ULL));
+    }
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)sum);
+}
+
+__global__ void gol_hash_bytes(const uint8_t* __restrict__ cells, int64_t W, int64_t H, unsigned long long* acc) {
+    const int64_t nc = (W + 63) / 64;
+    const int64_t n = nc * H;
+    uint64_t sum = 0;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = idx % nc, y = idx / nc;
+        uint64_t v = 0;
+        for (int b = 0; b < 64 && j * 64 + b < W; b++) v |= (uint64_t)(cells[y * W + j * 64 + b] != 0) << b;
+        sum += fmix64(v ^ fmix64((uint64_t)idx + 0x9E3779B97F4A7C15ULL));
+    }
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)sum);
+}
+
+// set the cells listed as (x, y) pairs (RLE placement); ilv == 0: byte board
+__global__ void gol_set_points(void* board, int ilv, int64_t W, int64_t pitch, const int64_t* xy, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t x = xy[2 * i], y = xy[2 * i + 1];
+    if (ilv > 0) {
+        int64_t word;
+        int bit;
+        cell_pos(x, ilv, word, bit);
+        atomicOr(&static_cast<uint32_t*>(board)[y * pitch + word], 1u << bit);
+    } else {
+        static_cast<uint8_t*>(board)[x + y * W] = 1;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Launchers (host).  Geometry was validated by the caller (gol_capi.cpp).
+
+static inline unsigned grid1d(int64_t n, int block = 256) {
+    int64_t g = (n + block - 1) / block;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+static inline unsigned grid_stride(int64_t n, int block = 256) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 8192) g = 8192;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s) {
+    if (bounded)
+        hipLaunchKernelGGL((gol_bytes_step<true>), dim3(grid1d(W * H)), dim3(256), 0, s, src, dst, W, H);
+    else
+        hipLaunchKernelGGL((gol_bytes_step<false>), dim3(grid1d(W * H)), dim3(256), 0, s, src, dst, W, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                       int ilv, hipStream_t s) {
+    hipLaunchKernelGGL(gol_pack, dim3(grid1d(W / 32 * rows)), dim3(256), 0, s, cells, words, W, rows, pitch, row0, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                         int64_t stride, uint8_t value, int ilv, hipStream_t s) {
+    hipLaunchKernelGGL(gol_unpack, dim3(grid1d(W / 32 * rows)), dim3(256), 0, s, words, out, W, rows, pitch, row0,
+                       stride, value, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_region(const void* board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
+                         int64_t h, uint8_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(gol_region, dim3(grid1d(w * h)), dim3(256), 0, s, board, ilv, W, pitch, x0, y0, w, h, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bytes_render(const uint8_t* cells, uint8_t* out, int64_t W, int64_t H, int64_t stride,
+                               uint8_t value, hipStream_t s) {
+    hipLaunchKernelGGL(gol_bytes_render, dim3(grid1d(W * H)), dim3(256), 0, s, cells, out, W, H, stride, value);
+    return hipGetLastError();
+}
+
+hipError_t launch_splitmix_packed(uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
+                                  int64_t gy0, uint64_t seed, int ilv, hipStream_t s) {
+    hipLaunchKernelGGL(gol_splitmix_packed, dim3(grid1d(wpr * rows)), dim3(256), 0, s, words, wpr, rows, pitch, row0,
+                       gy0, seed, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_splitmix_bytes(uint8_t* cells, int64_t W, int64_t H, uint64_t seed, hipStream_t s) {
+    hipLaunchKernelGGL(gol_splitmix_bytes, dim3(grid1d(W * H)), dim3(256), 0, s, cells, W, H, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_popcount_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
+                                  unsigned long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(gol_popcount_packed, dim3(grid_stride(wpr * rows)), dim3(256), 0, s, words, wpr, rows, pitch,
+                       row0, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_popcount_bytes(const uint8_t* cells, int64_t n, unsigned long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(gol_popcount_bytes, dim3(grid_stride(n)), dim3(256), 0, s, cells, n, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_packed(const uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                              int64_t gy0, int ilv, unsigned long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(gol_hash_packed, dim3(grid_stride((W + 63) / 64 * rows)), dim3(256), 0, s, words, W, rows, pitch,
+                       row0, gy0, ilv, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(gol_hash_bytes, dim3(grid_stride((W + 63) / 64 * H)), dim3(256), 0, s, cells, W, H, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, const int64_t* xy, int64_t n,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(gol_set_points, dim3(grid1d(n)), dim3(256), 0, s, board, ilv, W, pitch, xy, n);
+    return hipGetLastError();
+}
+
+}  // namespace gol

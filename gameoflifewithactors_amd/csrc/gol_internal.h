@@ -1,14 +1,14 @@
-// gol_internal.h -- launcher prototypes shared by gol_kernels.hip and gol_capi.cpp (not installed).
+// gol_internal.h -- launcher prototypes shared by the kernel files and gol_capi.cpp (not installed).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace gol {
 
-// Geometry of one streaming pass over a bit-packed buffer (see gol_kernels.hip).
+// Geometry of one streaming pass over a bit-packed buffer (gol_step.hip).
 struct StreamArgs {
     int64_t words;      // board words per row (board width / 32)
-    int64_t pitch;      // words per buffer row
+    int64_t pitch;      // words per buffer row (multiple of ilv)
     int64_t rows;       // owned rows (in wrap mode: all rows of the buffer)
     int64_t ghost;      // halo rows stored above and below the owned rows (0 in wrap mode)
     int64_t y0;         // global row index of owned row 0 (bounded masking, strips)
@@ -16,32 +16,42 @@ struct StreamArgs {
     int64_t out_begin;  // owned rows [out_begin, out_end) are produced
     int64_t out_end;
     int64_t seg;        // rows per wave segment (plan_stream)
-    int64_t nstrips;    // filled by the launcher
-    int64_t nsegs;      // filled by the launcher
+    int64_t nstrips;    // filled by plan_stream
+    int64_t nsegs;      // filled by plan_stream
+    int32_t ilv;        // words per interleaved block (gol_layout.h): 1, 2 or 4
+    int32_t pad_;
 };
 
-int64_t stream_strips(int64_t words);
+// ---- gol_step.hip
+bool stream_supported(int k, int ilv);
+int stream_max_k(int ilv);
+int stream_largest_k(int64_t n, int cap, int ilv);
+int64_t stream_strips(int64_t words, int ilv);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s);
+
+// ---- gol_formats.hip
 hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s);
 hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
-                       hipStream_t s);
+                       int ilv, hipStream_t s);
 hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
-                         int64_t stride, uint8_t value, hipStream_t s);
-hipError_t launch_region(const void* board, bool packed, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
-                          int64_t h, uint8_t* out, hipStream_t s);
+                         int64_t stride, uint8_t value, int ilv, hipStream_t s);
+hipError_t launch_region(const void* board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
+                         int64_t h, uint8_t* out, hipStream_t s);
 hipError_t launch_bytes_render(const uint8_t* cells, uint8_t* out, int64_t W, int64_t H, int64_t stride,
                                uint8_t value, hipStream_t s);
 hipError_t launch_splitmix_packed(uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
-                                  int64_t gy0, uint64_t seed, hipStream_t s);
+                                  int64_t gy0, uint64_t seed, int ilv, hipStream_t s);
 hipError_t launch_splitmix_bytes(uint8_t* cells, int64_t W, int64_t H, uint64_t seed, hipStream_t s);
 hipError_t launch_popcount_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
                                   unsigned long long* acc, hipStream_t s);
 hipError_t launch_popcount_bytes(const uint8_t* cells, int64_t n, unsigned long long* acc, hipStream_t s);
-hipError_t launch_hash_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
-                              int64_t gy0, unsigned long long* acc, hipStream_t s);
+hipError_t launch_hash_packed(const uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
+                              int64_t gy0, int ilv, unsigned long long* acc, hipStream_t s);
 hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s);
+hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, const int64_t* xy, int64_t n,
+                             hipStream_t s);
 
 }  // namespace gol

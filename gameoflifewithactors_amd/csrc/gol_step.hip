@@ -1,0 +1,421 @@
+// gol_step.hip -- the hot kernel: temporal-blocked streaming step of a bit-packed board on gfx950.
+//
+// Replaces one or more `updateView()` ticks of the reference (GameOfLifeDriver.fs:32-34), i.e. the
+// per-cell actor protocol of GameOfLifeLogic.fs:39-71 / GameofLife.fs:88-138, for all cells at once.
+//
+// Decomposition: one wavefront owns a column strip of 64 blocks (62 interior + one halo block per side;
+// lane = block of M words, gol_layout.h) and streams down a segment of rows.  Every row loaded from HBM
+// (one 4*M-byte vector load per lane) is pushed through K generations held in registers -- per
+// generation level a 3-row window of horizontal row sums -- so a pass reads and writes the board once
+// per K generations.  Neighbour words come from the lane's own registers (interleaved layout), the
+// block-edge words from the neighbouring lanes (DPP wave_shr:1 and ds_bpermute), bit carries from
+// v_alignbit_b32, counts from v_bitop3_b32 (gol_bitlogic.h).  No LDS arrays, no barriers, no atomics.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <cstdlib>
+
+#include "gol_bitlogic.h"
+#include "gol_internal.h"
+
+namespace gol {
+
+static constexpr int kWave = 64;
+static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip
+static constexpr int kWavesPerBlock = 4;
+
+// Cross-lane exchange of the block-edge words.  Measured on gfx950 (tools/ubench/valu_rates.hip,
+// profiles/r1/valu_rates_gfx950.jsonl): a DPP move costs a half-rate VALU issue slot; ds_bpermute_b32
+// runs on the LDS pipe (no VALU slot, longer latency).  GOL_XLANE:
+//   0 = DPP both directions, 1 = ds_bpermute both directions, 2 = left via DPP, right via ds_bpermute
+#ifndef GOL_XLANE
+#define GOL_XLANE 2
+#endif
+struct XLane {
+    int left_addr, right_addr;  // byte addresses of lane-1 / lane+1 for ds_bpermute
+    __device__ __forceinline__ explicit XLane(int lane)
+        : left_addr(((lane - 1) & 63) << 2), right_addr(((lane + 1) & 63) << 2) {}
+    __device__ __forceinline__ uint32_t from_left(uint32_t v) const {  // lane i <- lane i-1
+#if GOL_XLANE == 1
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(left_addr, (int)v);
+#else
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);  // wave_shr:1
+#endif
+    }
+    __device__ __forceinline__ uint32_t from_right(uint32_t v) const {  // lane i <- lane i+1
+#if GOL_XLANE == 0
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
+#else
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(right_addr, (int)v);
+#endif
+    }
+};
+
+__device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t m) {
+    int64_t r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+template <int M>
+struct Vec;
+template <>
+struct Vec<1> {
+    using T = uint32_t;
+    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[1]) { w[0] = t; }
+    __device__ __forceinline__ static T pack(const uint32_t (&w)[1]) { return w[0]; }
+};
+template <>
+struct Vec<2> {
+    using T = uint2;
+    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[2]) {
+        w[0] = t.x;
+        w[1] = t.y;
+    }
+    __device__ __forceinline__ static T pack(const uint32_t (&w)[2]) { return make_uint2(w[0], w[1]); }
+};
+template <>
+struct Vec<4> {
+    using T = uint4;
+    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[4]) {
+        w[0] = t.x;
+        w[1] = t.y;
+        w[2] = t.z;
+        w[3] = t.w;
+    }
+    __device__ __forceinline__ static T pack(const uint32_t (&w)[4]) { return make_uint4(w[0], w[1], w[2], w[3]); }
+};
+
+// Rows per loop trip (even, and a multiple of 4 so register roles repeat every trip): enough loads in
+// flight for the memory-bound K = 1 pass, fewer for the deep passes whose registers hold the windows.
+template <int K, int M>
+struct TripRows {
+    static constexpr int value = (K == 1 && M == 1) ? 8 : 4;
+};
+
+// One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+struct StreamWave {
+    static constexpr int R = TripRows<K, M>::value;
+    static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
+    using V = Vec<M>;
+    using VT = typename V::T;
+
+    const VT* __restrict__ src;
+    VT* __restrict__ dst;
+    const StreamArgs& a;
+    XLane xl;
+    uint32_t lc;       // this lane's block column (in units of M words)
+    uint32_t colmask;  // bounded: ~0 for an on-board block
+    bool store_lane;
+    int64_t pitch_v;  // buffer row pitch in blocks
+    int64_t seg_begin, seg_end, nsteps, ly0;
+    int64_t load_br;  // buffer row of the next level-0 row to load (uniform)
+
+    // level state: two row slots (X, Y) of block row sums (s, c) and the raw centre block of slot Y
+    uint32_t sX[K][M], cX[K][M], sY[K][M], cY[K][M], aY[K][M];
+
+    __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
+                                          int64_t sx, int64_t sy)
+        : src(reinterpret_cast<const VT*>(s)), dst(reinterpret_cast<VT*>(d)), a(args), xl(lane) {
+        const int64_t nblocks = a.words / M;
+        const int64_t cb = sx * kInterior - 1 + lane;  // this lane's block column (may be off-board)
+        if (BOUNDED) {
+            const bool in = cb >= 0 && cb < nblocks;
+            colmask = in ? 0xffffffffu : 0u;
+            lc = in ? (uint32_t)cb : 0u;
+        } else {
+            colmask = 0xffffffffu;
+            lc = (uint32_t)floor_mod(cb, nblocks);
+        }
+        store_lane = lane >= 1 && lane <= kInterior && cb < nblocks;
+        pitch_v = a.pitch / M;
+        seg_begin = a.out_begin + sy * a.seg;
+        seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
+        nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
+        ly0 = seg_begin - K;                     // level-0 row of step 0
+        load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
+#pragma unroll
+        for (int g = 0; g < K; g++)
+#pragma unroll
+            for (int j = 0; j < M; j++) sX[g][j] = cX[g][j] = sY[g][j] = cY[g][j] = aY[g][j] = 0;
+    }
+
+    // Load the next R level-0 rows.  Loads are unconditional (addresses clamped, values masked) so every
+    // trip issues a fixed number of memory operations and the compiler waits for exactly the loads.
+    __device__ __forceinline__ void load(uint32_t (&buf)[R][M], int64_t first_step) {
+        const int64_t buf_rows = a.rows + 2 * a.ghost;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            int64_t br = load_br;
+            if (WRAP_ROWS) {
+                load_br = br + 1 == a.rows ? 0 : br + 1;
+            } else {
+                load_br = br + 1;
+                // rows outside the buffer (beyond a bounded board's edge, or past the segment's last
+                // step) are never used unmasked: clamp the address into the buffer
+                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+            }
+            V::unpack(src[br * pitch_v + lc], buf[r]);
+            if (BOUNDED) {
+                const int64_t gy = a.y0 + ly0 + first_step + r;
+                const uint32_t m = (gy >= 0 && gy < a.height) ? colmask : 0u;
+#pragma unroll
+                for (int j = 0; j < M; j++) buf[r][j] &= m;
+            }
+        }
+    }
+
+    // One level, one row: window (prev P, centre C) + new row v -> next generation of the C row.
+    // The new row's sums overwrite the P slot (it becomes the centre slot of the following row).
+    __device__ __forceinline__ void level_row(uint32_t (&v)[M], uint32_t (&sP)[M], uint32_t (&cP)[M],
+                                              const uint32_t (&sC)[M], const uint32_t (&cC)[M],
+                                              const uint32_t (&alC)[M], uint32_t rowmask, uint32_t (&out)[M]) {
+        uint32_t sN[M], cN[M];
+        row_sum_block<M>(v, xl.from_left(v[M - 1]), xl.from_right(v[0]), sN, cN);
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
+            if (BOUNDED) out[j] &= rowmask;
+            sP[j] = sN[j];
+            cP[j] = cN[j];
+        }
+    }
+
+    // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
+    // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
+    template <bool SKIP>
+    __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
+        const int64_t lyt = ly0 + t * R;
+#pragma unroll
+        for (int g = 0; g < K; g++) {
+            if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
+                if (BOUNDED) {  // cells outside the board stay dead at every generation (Script.fsx:11)
+                    const int64_t gy = a.y0 + lyt + r - g - 1;  // row produced from v[r] at level g + 1
+                    m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
+                    m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
+                }
+                // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
+                uint32_t o0[M], o1[M];
+                level_row(v[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row(v[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1, o1);
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    aY[g][j] = v[r + 1][j];
+                    v[r][j] = o0[j];
+                    v[r + 1][j] = o1[j];
+                }
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row) {
+        dst[((WRAP_ROWS ? 0 : a.ghost) + row) * pitch_v + lc] = V::pack(v);
+    }
+    __device__ __forceinline__ void store_all(const uint32_t (&v)[R][M], int64_t t) {
+        const int64_t lo = ly0 + t * R - K;
+        if (store_lane) {
+#pragma unroll
+            for (int r = 0; r < R; r++) store_row(v[r], lo + r);
+        }
+    }
+    __device__ __forceinline__ void store_masked(const uint32_t (&v)[R][M], int64_t t) {
+        const int64_t lo = ly0 + t * R - K;
+        if (store_lane) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (lo + r >= seg_begin && lo + r < seg_end) store_row(v[r], lo + r);
+        }
+    }
+};
+
+// Trips: [0, t_fill) pipeline fill (no stores, garbage levels skipped), [t_fill, first_store_trip)
+// transition, [.., t_tail) steady state (every row stored, fixed memory-op count per trip), [t_tail,
+// ntrips) masked tail.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch).
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+__global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const uint32_t* __restrict__ src,
+                                                                          uint32_t* __restrict__ dst,
+                                                                          StreamArgs a) {
+    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS>;
+    constexpr int R = W::R;
+    const int lane = threadIdx.x & (kWave - 1);
+    // wave index made provably uniform so all row bookkeeping lives in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    if (gw >= a.nstrips * a.nsegs) return;
+    W w(src, dst, a, lane, gw % a.nstrips, gw / a.nstrips);
+
+    const int64_t ntrips = (w.nsteps + R - 1) / R;
+    const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
+    const int64_t first_store_trip = (2 * K + R - 1) / R;
+    int64_t t_tail = (2 * K + (w.seg_end - w.seg_begin)) / R;  // trips entirely inside the stored range
+    if (t_tail < first_store_trip) t_tail = first_store_trip;
+    if (t_tail > ntrips) t_tail = ntrips;
+
+    uint32_t nxt[R][M], v[R][M];
+    w.load(nxt, 0);
+    int64_t t = 0;
+    for (; t < t_fill; t++) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
+        w.load(nxt, (t + 1) * R);
+        w.template process<true>(v, t);
+    }
+    for (; t < first_store_trip && t < ntrips; t++) {  // transition trip (when R does not divide 2K)
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
+        w.load(nxt, (t + 1) * R);
+        w.template process<true>(v, t);
+        w.store_masked(v, t);
+    }
+    for (; t < t_tail; t++) {  // steady state
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
+        w.load(nxt, (t + 1) * R);
+        w.template process<false>(v, t);
+        w.store_all(v, t);
+    }
+    for (; t < ntrips; t++) {  // masked tail
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
+        w.load(nxt, (t + 1) * R);
+        w.template process<false>(v, t);
+        w.store_masked(v, t);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Supported (K, M) instantiations.  M = 1: any board with W % 32 == 0; M = 2 / 4 need W % 64 / 128.
+// Deeper K needs 5*M*K window registers per lane, so the deepest K shrinks as M grows.
+#define GOL_FOR_EACH_KM(X)                                                                               \
+    X(1, 1) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(24, 1) X(32, 1)                                           \
+    X(1, 2) X(2, 2) X(4, 2) X(8, 2) X(12, 2) X(16, 2)                                                    \
+    X(1, 4) X(2, 4) X(4, 4) X(6, 4) X(8, 4)
+
+bool stream_supported(int k, int ilv) {
+#define GOL_SUP(K_, M_) \
+    if (k == K_ && ilv == M_) return true;
+    GOL_FOR_EACH_KM(GOL_SUP)
+#undef GOL_SUP
+    return false;
+}
+
+int stream_max_k(int ilv) { return ilv == 1 ? 32 : (ilv == 2 ? 16 : 8); }
+
+int stream_largest_k(int64_t n, int cap, int ilv) {
+    static const int ks[] = {32, 24, 16, 12, 8, 6, 4, 2, 1};
+    for (int k : ks)
+        if (k <= cap && k <= n && stream_supported(k, ilv)) return k;
+    return 1;
+}
+
+// Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
+// (never wraps: rows beyond the board are masked dead).
+template <int K, int M>
+static const void* stream_kernel(bool bounded, bool wrap) {
+    if (bounded) return (const void*)&gol_stream_step<K, M, true, false>;
+    return wrap ? (const void*)&gol_stream_step<K, M, false, true> : (const void*)&gol_stream_step<K, M, false, false>;
+}
+
+static const void* kernel_for(int k, int ilv, bool bounded, bool wrap) {
+#define GOL_KPTR(K_, M_) \
+    if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap);
+    GOL_FOR_EACH_KM(GOL_KPTR)
+#undef GOL_KPTR
+    return nullptr;
+}
+
+int64_t stream_strips(int64_t words, int ilv) { return (words / ilv + kInterior - 1) / kInterior; }
+
+// Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.
+// Falls back to 4096 when no device answers (host-only planning, e.g. CPU tests).
+static int64_t resident_waves(int k, int ilv, bool bounded, bool wrap) {
+    static std::atomic<int64_t> cache[33][5][2][2];
+    if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return 4096;
+    if (bounded) wrap = false;
+    int64_t v = cache[k][ilv][bounded][wrap].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    const void* fn = kernel_for(k, ilv, bounded, wrap);
+    int dev = 0, cus = 0, blocks = 0;
+    if (!fn || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kWave * kWavesPerBlock, 0) != hipSuccess ||
+        blocks <= 0 || cus <= 0) {
+        (void)hipGetLastError();
+        return 4096;
+    }
+    v = (int64_t)blocks * cus * kWavesPerBlock;
+    cache[k][ilv][bounded][wrap].store(v, std::memory_order_relaxed);
+    return v;
+}
+
+// Work decomposition: nstrips column strips x nsegs row segments, one wave each.  The segment count
+// makes the grid ONE balanced round of resident waves (a partial second round would leave a tail of
+// lone waves), with segments no shorter than 2K rows (pipeline fill cost).  GOL_SEG_ROWS overrides the
+// segment length (experiments).
+void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
+    static const int64_t env_seg = [] {
+        const char* e = std::getenv("GOL_SEG_ROWS");
+        return e ? std::atoll(e) : 0LL;
+    }();
+    a.nstrips = stream_strips(a.words, a.ilv);
+    const int64_t rows = a.out_end - a.out_begin;
+    if (rows <= 0) {
+        a.nsegs = 0;
+        a.seg = 1;
+        return;
+    }
+    int64_t seg = env_seg;
+    if (seg <= 0) {
+        const int64_t slots = resident_waves(k, a.ilv, bounded, wrap);
+        int64_t nsegs = slots / a.nstrips;
+        if (nsegs < 1) nsegs = 1;
+        const int64_t min_seg = 2 * k > 16 ? 2 * k : 16;
+        const int64_t max_segs = rows / min_seg > 0 ? rows / min_seg : 1;
+        if (nsegs > max_segs) nsegs = max_segs;
+        seg = (rows + nsegs - 1) / nsegs;
+    }
+    a.seg = seg;
+    a.nsegs = (rows + seg - 1) / seg;
+}
+
+template <int K, int M>
+static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
+                            hipStream_t s) {
+    const int64_t waves = a.nstrips * a.nsegs;
+    const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    const dim3 block(kWave * kWavesPerBlock);
+    if (bounded) {
+        hipLaunchKernelGGL((gol_stream_step<K, M, true, false>), dim3(blocks), block, 0, s, src, dst, a);
+    } else {
+        if (wrap)
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, true>), dim3(blocks), block, 0, s, src, dst, a);
+        else
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
+                              hipStream_t s) {
+    plan_stream(a, k, bounded, wrap);
+    if (a.nsegs <= 0) return hipSuccess;
+#define GOL_LAUNCH(K_, M_) \
+    if (k == K_ && a.ilv == M_) return launch_km<K_, M_>(src, dst, a, bounded, wrap, s);
+    GOL_FOR_EACH_KM(GOL_LAUNCH)
+#undef GOL_LAUNCH
+    return hipErrorInvalidValue;
+}
+
+}  // namespace gol

@@ -52,10 +52,11 @@ class Geometry:
     pitch: int
     boundary: int
     wrap_rows: bool
+    ilv: int = 1  # words per interleaved block (include/gol/gol.h, gol_strip.ilv)
 
     def strip(self) -> Strip:
         return Strip(self.width, self.height, self.y0, self.rows, self.ghost, self.pitch, self.boundary,
-                     1 if self.wrap_rows else 0)
+                     1 if self.wrap_rows else 0, self.ilv, 0)
 
     @property
     def buffer_rows(self) -> int:
@@ -68,6 +69,18 @@ class HipEngine:
     def __init__(self, device: torch.device):
         self.lib = _lib.load()
         self.device = device
+
+    def ilv_for(self, width: int) -> int:
+        return int(self.lib.gol_default_ilv(width))
+
+    def supports_k(self, k: int, ilv: int) -> bool:
+        return bool(self.lib.gol_supported_k(k, ilv))
+
+    def largest_k(self, n: int, cap: int, ilv: int) -> int:
+        for k in (32, 24, 16, 12, 8, 6, 4, 2, 1):
+            if k <= cap and k <= n and self.supports_k(k, ilv):
+                return k
+        return 1
 
     def alloc(self, geom: Geometry) -> torch.Tensor:
         return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32, device=self.device)
@@ -125,8 +138,11 @@ class StripRunner:
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.engine = engine if engine is not None else HipEngine(self.device)
         single = world == 1
+        ilv = getattr(self.engine, "ilv_for", lambda w: 1)(width)
+        if not getattr(self.engine, "supports_k", lambda kk, m: True)(k, ilv):
+            raise ValueError(f"temporal block k={k} is not supported for interleave {ilv}")
         self.geom = Geometry(width, height, y0, rows, 0 if single else k, width // 32, boundary,
-                             wrap_rows=single and boundary == TORUS)
+                             wrap_rows=single and boundary == TORUS, ilv=ilv)
         self.bufs = [self.engine.alloc(self.geom), self.engine.alloc(self.geom)]
         self.cur = 0
         self.generation = 0
@@ -183,9 +199,13 @@ class StripRunner:
 
     def step(self, generations: int) -> None:
         while generations > 0:
-            k = self.k if generations >= self.k else _largest_k(generations)
+            k = self.k if generations >= self.k else self._largest_k(generations)
             self.step_pass(k)
             generations -= k
+
+    def _largest_k(self, n: int) -> int:
+        fn = getattr(self.engine, "largest_k", None)
+        return fn(n, self.k, self.geom.ilv) if fn else _largest_k(n)
 
     def launches_per_pass(self) -> int:
         return 1 if self.world == 1 else 3
@@ -282,7 +302,7 @@ class LocalBoard:
 
     def step(self, generations: int) -> None:
         while generations > 0:
-            k = self.k if generations >= self.k else _largest_k(generations)
+            k = self.k if generations >= self.k else self.runners[0]._largest_k(generations)
             self.step_pass(k)
             generations -= k
 

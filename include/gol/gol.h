@@ -48,7 +48,8 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  * Dictionary never reaches 8 keys and the board freezes, GameOfLifeLogic.fs:58 -- rejected here).
  * boundary: GOL_TORUS (actors, GameOfLifeDriver.fs:25) or GOL_BOUNDED (Script.fsx:11).
  * num_gpus: must be 1 in this build (multi-GPU runs use one process per GPU, gol_strip_*).
- * tblock_k: generations fused per pass (0 = default 16; one of 1,2,4,8,16,24,32).
+ * tblock_k: upper bound on the generations fused per kernel pass (0 = the layout's default; else one of
+ *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
  * The initial board is all dead. */
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
 int gol_destroy(gol_board* b);
@@ -85,6 +86,13 @@ int gol_hash(gol_board* b, uint64_t* out); /* canonical 64-bit board hash (DESIG
 
 /* Introspection: width, height, boundary, tblock_k, packed (1 = bit-packed path, 0 = byte path). */
 int gol_info(gol_board* b, int64_t* width, int64_t* height, int* boundary, int* tblock_k, int* packed);
+/* Packed layout of the board: ilv = words per interleaved block (1, 2, 4; 0 = byte board), pitch in words. */
+int gol_layout(gol_board* b, int* ilv, int64_t* pitch);
+/* Layout / depth the engine picks for a width (0 if the width is not a multiple of 32), the default
+ * temporal-block depth for a layout, and whether the step kernel supports depth k for a layout. */
+int gol_default_ilv(int64_t width);
+int gol_default_tblock(int ilv);
+int gol_supported_k(int k, int ilv);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller. */
 int gol_stream(gol_board* b, void** stream);
 
@@ -95,8 +103,9 @@ const char* gol_version(void);
  * Row-strip entry points for multi-GPU runs (one process per GPU; the caller owns device memory and
  * does the halo exchange, e.g. RCCL send/recv).  A strip buffer holds `ghost` halo rows, then `rows`
  * owned rows (global rows [y0, y0+rows)), then `ghost` halo rows; each buffer row is `pitch` 32-bit
- * words, of which the first width/32 are the board row (bit b of word w = cell x = 32w + b).
- * width must be a multiple of 32.  With world size 1 a strip may instead set wrap_rows = 1, ghost = 0,
+ * words, of which the first width/32 are the board row in the interleaved layout `ilv`:
+ *     row = blocks of ilv words; in block k, word j bit b = cell x = 32*ilv*k + j + ilv*b
+ * (ilv = 1: bit b of word w = cell 32w + b).  width must be a multiple of 32*ilv, pitch of ilv.  With world size 1 a strip may instead set wrap_rows = 1, ghost = 0,
  * rows = height: torus rows then wrap inside the buffer (the single-GPU board layout).
  * `stream` is a hipStream_t (NULL = default stream).  All calls are asynchronous. */
 typedef struct gol_strip {
@@ -108,6 +117,8 @@ typedef struct gol_strip {
     int64_t pitch;    /* words per buffer row (>= width/32) */
     int32_t boundary; /* GOL_TORUS | GOL_BOUNDED */
     int32_t wrap_rows;
+    int32_t ilv;      /* words per interleaved block: 1, 2 or 4 (gol_default_ilv) */
+    int32_t reserved; /* 0 */
 } gol_strip;
 
 /* k generations over owned rows [out_begin, out_end) from src to dst (distinct buffers, same geometry).

@@ -13,22 +13,36 @@ import torch
 import gol_oracle as o
 
 
-def _unpack(words: np.ndarray, width: int) -> np.ndarray:
-    """(rows, pitch) int32 -> (rows, width) uint8, bit b of word w = cell 32w + b."""
-    b = np.unpackbits(words.astype("<u4").view(np.uint8), axis=1, bitorder="little")
-    return b[:, :width].copy()
+def _cell_of_bit(width: int, ilv: int) -> np.ndarray:
+    """For every stored bit position p = 32*w + b of a row: the cell it holds (include/gol/gol.h layout:
+    block k of ilv words, word j bit b = cell 32*ilv*k + j + ilv*b)."""
+    p = np.arange(width)
+    w, b = p // 32, p % 32
+    return (w // ilv) * 32 * ilv + (w % ilv) + ilv * b
 
 
-def _pack(cells: np.ndarray, pitch: int) -> np.ndarray:
+def _unpack(words: np.ndarray, width: int, ilv: int = 1) -> np.ndarray:
+    """(rows, pitch) int32 -> (rows, width) uint8 cells."""
+    bits = np.unpackbits(words.astype("<u4").view(np.uint8), axis=1, bitorder="little")[:, :width]
+    out = np.empty_like(bits)
+    out[:, _cell_of_bit(width, ilv)] = bits
+    return out
+
+
+def _pack(cells: np.ndarray, pitch: int, ilv: int = 1) -> np.ndarray:
     rows, width = cells.shape
     padded = np.zeros((rows, pitch * 32), np.uint8)
-    padded[:, :width] = cells
+    padded[:, :width] = cells[:, _cell_of_bit(width, ilv)]
     return np.packbits(padded, axis=1, bitorder="little").view("<u4").astype(np.uint32).view(np.int32)
 
 
 class OracleEngine:
-    def __init__(self, device=None):
+    def __init__(self, device=None, ilv: int = 1):
         self.device = torch.device("cpu")
+        self.ilv = ilv
+
+    def ilv_for(self, width):
+        return self.ilv
 
     def alloc(self, geom):
         return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32)
@@ -52,25 +66,25 @@ class OracleEngine:
             words = src.numpy()[rows]
         else:
             words = src.numpy()[lo + g:hi + g]
-        cells = _unpack(words, geom.width)
+        cells = _unpack(words, geom.width, geom.ilv)
         # torus in x is exact; the array's y edges that are not board edges only pollute rows inside
         # the k-row light cone that is discarded below
         res = o.c_run(cells, k, geom.boundary)
         out = res[out_begin - lo:out_end - lo]
-        dst.numpy()[out_begin + g:out_end + g] = _pack(out, geom.pitch)
+        dst.numpy()[out_begin + g:out_end + g] = _pack(out, geom.pitch, geom.ilv)
 
     def seed_splitmix(self, geom, buf, seed, stream=None):
         full = o.seed_splitmix(geom.width, geom.height, seed)
-        buf.numpy()[geom.ghost:geom.ghost + geom.rows] = _pack(full[geom.y0:geom.y0 + geom.rows], geom.pitch)
+        buf.numpy()[geom.ghost:geom.ghost + geom.rows] = _pack(full[geom.y0:geom.y0 + geom.rows], geom.pitch, geom.ilv)
 
     def set_cells(self, geom, buf, cells_u8, stream=None):
-        buf.numpy()[geom.ghost:geom.ghost + geom.rows] = _pack(np.asarray(cells_u8, np.uint8), geom.pitch)
+        buf.numpy()[geom.ghost:geom.ghost + geom.rows] = _pack(np.asarray(cells_u8, np.uint8), geom.pitch, geom.ilv)
 
     def get_cells(self, geom, buf, stream=None):
-        return torch.from_numpy(_unpack(buf.numpy()[geom.ghost:geom.ghost + geom.rows], geom.width))
+        return torch.from_numpy(_unpack(buf.numpy()[geom.ghost:geom.ghost + geom.rows], geom.width, geom.ilv))
 
     def reduce(self, geom, buf, what, stream=None):
-        cells = _unpack(buf.numpy()[geom.ghost:geom.ghost + geom.rows], geom.width)
+        cells = _unpack(buf.numpy()[geom.ghost:geom.ghost + geom.rows], geom.width, geom.ilv)
         if what != "hash":
             return torch.tensor([int(cells.sum())], dtype=torch.int64)
         nc = (geom.width + 63) // 64

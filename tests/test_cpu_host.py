@@ -44,6 +44,15 @@ def test_library_exports_every_declared_symbol():
         assert name in _lib.SIGNATURES, f"_lib.SIGNATURES lacks a binding for {name}"
 
 
+def test_layout_choice():
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    assert [lib.gol_default_ilv(w) for w in (100, 32, 96, 64, 320, 128, 65536)] == [0, 1, 1, 2, 2, 4, 4]
+    assert all(lib.gol_supported_k(lib.gol_default_tblock(m), m) for m in (1, 2, 4))
+    assert lib.gol_supported_k(16, 4) == 0 and lib.gol_supported_k(32, 1) == 1
+
+
 def test_library_reports_version_without_gpu():
     from gameoflifewithactors_amd import _lib
 
@@ -103,12 +112,19 @@ def test_strip_validation_without_gpu():
     from gameoflifewithactors_amd import _lib
 
     lib = _lib.load()
-    s = _lib.Strip(width=96, height=10, y0=0, rows=10, ghost=0, pitch=3, boundary=0, wrap_rows=0)
+    s = _lib.Strip(width=96, height=10, y0=0, rows=10, ghost=0, pitch=3, boundary=0, wrap_rows=0, ilv=1)
     w, seg = ctypes.c_int64(), ctypes.c_int64()
     assert lib.gol_strip_plan(ctypes.byref(s), 4, 0, 10, ctypes.byref(w), ctypes.byref(seg)) == 0
     assert w.value == 1 and seg.value == 10  # 3 words -> 1 column strip; 10 rows -> 1 segment
-    bad = _lib.Strip(width=100, height=10, y0=0, rows=10, ghost=0, pitch=4, boundary=0, wrap_rows=0)
+    bad = _lib.Strip(width=100, height=10, y0=0, rows=10, ghost=0, pitch=4, boundary=0, wrap_rows=0, ilv=1)
     assert lib.gol_strip_plan(ctypes.byref(bad), 4, 0, 10, None, None) == _lib.GOL_ERR_INVALID
+    for ilv, width in ((3, 96), (4, 96), (2, 96)):  # ilv must be 1/2/4 and divide the row into blocks
+        bad = _lib.Strip(width=width, height=10, y0=0, rows=10, ghost=0, pitch=3, boundary=0, wrap_rows=0, ilv=ilv)
+        assert lib.gol_strip_plan(ctypes.byref(bad), 4, 0, 10, None, None) == _lib.GOL_ERR_INVALID
+    # depth 16 exists for ilv 1 and 2 but not 4 (window registers: 5 * ilv * k per lane)
+    s4 = _lib.Strip(width=256, height=64, y0=0, rows=64, ghost=0, pitch=8, boundary=0, wrap_rows=0, ilv=4)
+    assert lib.gol_strip_plan(ctypes.byref(s4), 16, 0, 64, None, None) == _lib.GOL_ERR_INVALID
+    assert lib.gol_strip_plan(ctypes.byref(s4), 8, 0, 64, None, None) == 0
     # a k-generation pass needs k ghost rows when rows do not wrap
     dummy = ctypes.c_void_p(16)
     assert lib.gol_strip_step(ctypes.byref(s), dummy, ctypes.c_void_p(32), 4, 0, 10, None) == _lib.GOL_ERR_INVALID

@@ -14,7 +14,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-KS = [1, 2, 4, 8, 16, 24, 32]
+KS = [1, 2, 4, 6, 8, 12, 16, 24, 32]  # caps: each layout uses its deepest supported depth <= k
 
 
 @pytest.fixture(scope="module")

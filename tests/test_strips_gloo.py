@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, width, height, boundary, k, gens, seed, q):
+def _worker(rank, world, port, width, height, boundary, k, gens, seed, q, ilv=1):
     import sys
 
     sys.path.insert(0, HERE)
@@ -35,7 +35,7 @@ def _worker(rank, world, port, width, height, boundary, k, gens, seed, q):
         from gameoflifewithactors_amd.strips import StripRunner
 
         r = StripRunner(width, height, boundary, k, rank=rank, world=world, device=torch.device("cpu"),
-                        engine=OracleEngine())
+                        engine=OracleEngine(ilv=ilv))
         r.seed_splitmix(seed)
         r.step(gens)
         h = r.hash()
@@ -49,14 +49,16 @@ def _worker(rank, world, port, width, height, boundary, k, gens, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,boundary,k,gens,height", [(2, 0, 4, 13, 40), (2, 1, 4, 13, 40), (3, 0, 8, 20, 50),
-                                                          (3, 1, 2, 9, 31), (2, 0, 16, 32, 35)])
-def test_strip_protocol_matches_oracle(oracle, world, boundary, k, gens, height):
-    width, seed = 96, 0x5EED
+@pytest.mark.parametrize("world,boundary,k,gens,height,ilv", [(2, 0, 4, 13, 40, 1), (2, 1, 4, 13, 40, 1),
+                                                              (3, 0, 8, 20, 50, 1), (3, 1, 2, 9, 31, 1),
+                                                              (2, 0, 16, 32, 35, 1), (2, 0, 8, 19, 40, 4),
+                                                              (3, 1, 4, 11, 33, 2)])
+def test_strip_protocol_matches_oracle(oracle, world, boundary, k, gens, height, ilv):
+    width, seed = 256, 0x5EED
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, width, height, boundary, k, gens, seed, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, width, height, boundary, k, gens, seed, q, ilv))
              for r in range(world)]
     for p in procs:
         p.start()

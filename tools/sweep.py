@@ -22,11 +22,15 @@ def main():
     a = p.parse_args()
     import torch
 
-    from gameoflifewithactors_amd import Board
+    from gameoflifewithactors_amd import Board, _lib
 
     W = a.size
     H = a.height or a.size
+    lib = _lib.load()
+    ilv = lib.gol_default_ilv(W)  # honours GOL_ILV
     for k in [int(x) for x in a.ks.split(",")]:
+        if not lib.gol_supported_k(k, ilv):
+            continue
         with Board(W, H, a.boundary, tblock_k=k) as b:
             b.seed_splitmix(0x5EED)
             s = torch.cuda.ExternalStream(b.stream)
@@ -39,9 +43,9 @@ def main():
             b.synchronize()
             t = e0.elapsed_time(e1) / 1e3 / a.passes
             gcups = W * H * k / t / 1e9
-            print(json.dumps({"W": W, "H": H, "k": k, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
+            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
                               "alg_GBps": round(W * H / 4 / t / 1e9, 1),
-                              "valu_Tops": round(13 * W * H / 32 * k / t / 1e12, 2)}), flush=True)
+                              }), flush=True)
 
 
 if __name__ == "__main__":
