@@ -67,6 +67,8 @@ sp = ctypes.POINTER(Strip)
 # name -> (restype, argtypes).  Must cover every function include/gol/gol.h declares.
 SIGNATURES = {
     "gol_create": (ctypes.c_int, [i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+    "gol_create_ex": (ctypes.c_int, [i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(vp)]),
     "gol_destroy": (ctypes.c_int, [vp]),
     "gol_set_cells": (ctypes.c_int, [vp, u8p, i64]),
     "gol_get_cells": (ctypes.c_int, [vp, u8p, i64]),

@@ -30,13 +30,16 @@ class Board:
     """A width x height Life board on the current HIP device.
 
     boundary: ``TORUS`` (the actors' topology, GameOfLifeDriver.fs:25) or ``BOUNDED`` (Script.fsx:11).
-    tblock_k: generations fused per kernel pass (0 = library default).
+    tblock_k: upper bound on the generations fused per kernel pass (0 = library default).
+    ilv: packed layout, words per interleaved block (0 = library default for the width; 1, 2, 4).
     """
 
-    def __init__(self, width: int, height: int, boundary: int = TORUS, tblock_k: int = 0, num_gpus: int = 1):
+    def __init__(self, width: int, height: int, boundary: int = TORUS, tblock_k: int = 0, num_gpus: int = 1,
+                 ilv: int = 0):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
-        check(self._lib.gol_create(width, height, boundary, num_gpus, tblock_k, ctypes.byref(h)), "gol_create")
+        check(self._lib.gol_create_ex(width, height, boundary, num_gpus, tblock_k, ilv, ctypes.byref(h)),
+              "gol_create")
         self._h = h
         self.width, self.height, self.boundary = width, height, boundary
 
@@ -128,7 +131,10 @@ class Board:
         w, h = ctypes.c_int64(), ctypes.c_int64()
         b, k, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(self._lib.gol_info(self._h, *(ctypes.byref(x) for x in (w, h, b, k, p))), "gol_info")
-        return {"width": w.value, "height": h.value, "boundary": b.value, "tblock_k": k.value, "packed": bool(p.value)}
+        ilv, pitch = ctypes.c_int(), ctypes.c_int64()
+        check(self._lib.gol_layout(self._h, ctypes.byref(ilv), ctypes.byref(pitch)), "gol_layout")
+        return {"width": w.value, "height": h.value, "boundary": b.value, "tblock_k": k.value, "packed": bool(p.value),
+                "ilv": ilv.value, "pitch": pitch.value}
 
     @property
     def stream(self) -> int:

@@ -122,21 +122,22 @@ bool valid_k(int k) {
     return k == 1 || k == 2 || k == 4 || k == 6 || k == 8 || k == 12 || k == 16 || k == 24 || k == 32;
 }
 
-// Interleave for a packed board of this width: the widest block that divides the row (gol_layout.h).
-// GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
+// Interleave for a packed board of this width (gol_layout.h).  Measured on MI355X at 65536^2
+// (profiles/r1/sweep_ilv.log): ilv 2 with K = 12 is the fastest configuration, ilv 4 needs 240 window
+// VGPRs at K = 8 (2 waves/SIMD) and wastes 1/9 of its lanes on a 65536-wide row, ilv 1 pays 4x the
+// funnel shifts.  GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
 int pick_ilv(int64_t width) {
     static const int env = [] {
         const char* e = std::getenv("GOL_ILV");
         return e ? std::atoi(e) : 0;
     }();
     if ((env == 1 || env == 2 || env == 4) && width % (32 * env) == 0) return env;
-    if (width % 128 == 0) return 4;
     if (width % 64 == 0) return 2;
     return 1;
 }
 
 // Default generations per pass for a layout (measured on MI355X, DESIGN.md "Temporal block depth").
-int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 16 : 24); }
+int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 24); }
 
 }  // namespace
 
@@ -343,6 +344,11 @@ uint64_t gol_hash_finalize(uint64_t h, int64_t width, int64_t height) {
 }
 
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out) {
+    return gol_create_ex(width, height, boundary, num_gpus, tblock_k, 0, out);
+}
+
+int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, int ilv,
+                  gol_board** out) {
     try {
         if (!out) return fail(GOL_ERR_INVALID, "null out");
         *out = nullptr;
@@ -355,6 +361,8 @@ int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tb
             return fail(GOL_ERR_UNSUPPORTED, "num_gpus must be 1; multi-GPU runs use one process per GPU (gol_strip_*)");
         if (tblock_k != 0 && !valid_k(tblock_k))
             return fail(GOL_ERR_INVALID, "tblock_k must be 0 (default) or one of 1,2,4,6,8,12,16,24,32");
+        if (ilv != 0 && ((ilv != 1 && ilv != 2 && ilv != 4) || width % (32 * ilv)))
+            return fail(GOL_ERR_INVALID, "ilv must be 0 (auto) or 1, 2, 4 dividing the width into 32*ilv-cell blocks");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(GOL_ERR_NO_DEVICE, "no HIP device");
         gol_board* b = new gol_board();
@@ -363,7 +371,7 @@ int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tb
         b->boundary = boundary;
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
-        b->ilv = b->packed ? pick_ilv(width) : 0;
+        b->ilv = b->packed ? (ilv ? ilv : pick_ilv(width)) : 0;
         b->tblock = tblock_k ? tblock_k : default_tblock(b->ilv);
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = hipGetDevice(&b->device);

@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gol_bitlogic.h"
 #include "gol_internal.h"
@@ -31,6 +32,10 @@ static constexpr int kWavesPerBlock = 4;
 //   0 = DPP both directions, 1 = ds_bpermute both directions, 2 = left via DPP, right via ds_bpermute
 #ifndef GOL_XLANE
 #define GOL_XLANE 2
+#endif
+// GOL_BATCH_XLANE: issue a level's ds_bpermute exchanges for all rows of a trip before its arithmetic
+#ifndef GOL_BATCH_XLANE
+#define GOL_BATCH_XLANE 1
 #endif
 struct XLane {
     int left_addr, right_addr;  // byte addresses of lane-1 / lane+1 for ds_bpermute
@@ -57,34 +62,58 @@ __device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t m) {
     return r < 0 ? r + m : r;
 }
 
+// Buffer-resource memory access: one uniform descriptor per row (SGPRs) + a 32-bit per-lane byte offset.
+// Offsets past num_records are dropped by the hardware range check, so lanes that must not store (halo
+// lanes, off-board blocks) store without a branch and every trip issues the same number of memory
+// operations -- which lets the compiler wait for exactly the prefetched loads (vmcnt counts stores too).
+static constexpr int kNoStore = 0x7ffffff0;  // offset beyond any row: store dropped
+static constexpr int kRsrcWord3 = 0x00020000;  // raw buffer, 32-bit data format (gfx9-family)
+static constexpr int kWaitVm0 = 0x0F70;        // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left at max)
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 template <int M>
 struct Vec;
 template <>
 struct Vec<1> {
-    using T = uint32_t;
-    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[1]) { w[0] = t; }
-    __device__ __forceinline__ static T pack(const uint32_t (&w)[1]) { return w[0]; }
+    __device__ __forceinline__ static void load(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&w)[1]) {
+        w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    }
+    __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, int off, const uint32_t (&w)[1]) {
+        __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, 0);
+    }
 };
 template <>
 struct Vec<2> {
-    using T = uint2;
-    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[2]) {
+    __device__ __forceinline__ static void load(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&w)[2]) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
         w[0] = t.x;
         w[1] = t.y;
     }
-    __device__ __forceinline__ static T pack(const uint32_t (&w)[2]) { return make_uint2(w[0], w[1]); }
+    __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, int off, const uint32_t (&w)[2]) {
+        const u32x2 t = {w[0], w[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(t, r, off, 0, 0);
+    }
 };
 template <>
 struct Vec<4> {
-    using T = uint4;
-    __device__ __forceinline__ static void unpack(const T& t, uint32_t (&w)[4]) {
+    __device__ __forceinline__ static void load(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&w)[4]) {
+        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
         w[0] = t.x;
         w[1] = t.y;
         w[2] = t.z;
         w[3] = t.w;
     }
-    __device__ __forceinline__ static T pack(const uint32_t (&w)[4]) { return make_uint4(w[0], w[1], w[2], w[3]); }
+    __device__ __forceinline__ static void store(__amdgpu_buffer_rsrc_t r, int off, const uint32_t (&w)[4]) {
+        const u32x4 t = {w[0], w[1], w[2], w[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(t, r, off, 0, 0);
+    }
 };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint32_t* row, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(row), (short)0, (int)bytes, kRsrcWord3);
+}
 
 // Rows per loop trip (even, and a multiple of 4 so register roles repeat every trip): enough loads in
 // flight for the memory-bound K = 1 pass, fewer for the deep passes whose registers hold the windows.
@@ -99,16 +128,15 @@ struct StreamWave {
     static constexpr int R = TripRows<K, M>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
     using V = Vec<M>;
-    using VT = typename V::T;
 
-    const VT* __restrict__ src;
-    VT* __restrict__ dst;
+    const uint32_t* __restrict__ src;
+    uint32_t* __restrict__ dst;
     const StreamArgs& a;
     XLane xl;
-    uint32_t lc;       // this lane's block column (in units of M words)
+    int load_off;      // this lane's byte offset in a row (its block column)
+    int store_off;     // = load_off for interior on-board lanes, kNoStore otherwise
     uint32_t colmask;  // bounded: ~0 for an on-board block
-    bool store_lane;
-    int64_t pitch_v;  // buffer row pitch in blocks
+    int64_t row_bytes;
     int64_t seg_begin, seg_end, nsteps, ly0;
     int64_t load_br;  // buffer row of the next level-0 row to load (uniform)
 
@@ -117,19 +145,21 @@ struct StreamWave {
 
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
                                           int64_t sx, int64_t sy)
-        : src(reinterpret_cast<const VT*>(s)), dst(reinterpret_cast<VT*>(d)), a(args), xl(lane) {
+        : src(s), dst(d), a(args), xl(lane) {
         const int64_t nblocks = a.words / M;
         const int64_t cb = sx * kInterior - 1 + lane;  // this lane's block column (may be off-board)
+        int64_t lc;
         if (BOUNDED) {
             const bool in = cb >= 0 && cb < nblocks;
             colmask = in ? 0xffffffffu : 0u;
-            lc = in ? (uint32_t)cb : 0u;
+            lc = in ? cb : 0;
         } else {
             colmask = 0xffffffffu;
-            lc = (uint32_t)floor_mod(cb, nblocks);
+            lc = floor_mod(cb, nblocks);
         }
-        store_lane = lane >= 1 && lane <= kInterior && cb < nblocks;
-        pitch_v = a.pitch / M;
+        load_off = (int)(lc * 4 * M);
+        store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
+        row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
@@ -156,7 +186,7 @@ struct StreamWave {
                 // step) are never used unmasked: clamp the address into the buffer
                 br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
-            V::unpack(src[br * pitch_v + lc], buf[r]);
+            V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
             if (BOUNDED) {
                 const int64_t gy = a.y0 + ly0 + first_step + r;
                 const uint32_t m = (gy >= 0 && gy < a.height) ? colmask : 0u;
@@ -168,11 +198,12 @@ struct StreamWave {
 
     // One level, one row: window (prev P, centre C) + new row v -> next generation of the C row.
     // The new row's sums overwrite the P slot (it becomes the centre slot of the following row).
-    __device__ __forceinline__ void level_row(uint32_t (&v)[M], uint32_t (&sP)[M], uint32_t (&cP)[M],
+    __device__ __forceinline__ void level_row(uint32_t (&v)[M], uint32_t left, uint32_t right, uint32_t (&sP)[M],
+                                              uint32_t (&cP)[M],
                                               const uint32_t (&sC)[M], const uint32_t (&cC)[M],
                                               const uint32_t (&alC)[M], uint32_t rowmask, uint32_t (&out)[M]) {
         uint32_t sN[M], cN[M];
-        row_sum_block<M>(v, xl.from_left(v[M - 1]), xl.from_right(v[0]), sN, cN);
+        row_sum_block<M>(v, left, right, sN, cN);
 #pragma unroll
         for (int j = 0; j < M; j++) {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
@@ -190,6 +221,14 @@ struct StreamWave {
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
+            // block-edge words of the right-hand lanes for all R rows first: the LDS-pipe exchanges
+            // (ds_bpermute) then overlap each other and the arithmetic below instead of each stalling
+            // its own row; the DPP (VALU) moves from the left stay next to their use
+            uint32_t right[R];
+#if GOL_BATCH_XLANE
+#pragma unroll
+            for (int r = 0; r < R; r++) right[r] = xl.from_right(v[r][0]);
+#endif
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
@@ -200,8 +239,13 @@ struct StreamWave {
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-                level_row(v[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-                level_row(v[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1, o1);
+#if !GOL_BATCH_XLANE
+                right[r] = xl.from_right(v[r][0]);
+                right[r + 1] = xl.from_right(v[r + 1][0]);
+#endif
+                level_row(v[r], xl.from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row(v[r + 1], xl.from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
+                          o1);
 #pragma unroll
                 for (int j = 0; j < M; j++) {
                     aY[g][j] = v[r + 1][j];
@@ -212,29 +256,25 @@ struct StreamWave {
         }
     }
 
-    __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row) {
-        dst[((WRAP_ROWS ? 0 : a.ghost) + row) * pitch_v + lc] = V::pack(v);
+    __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
+        V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? row_bytes : 0), store_off, v);
     }
-    __device__ __forceinline__ void store_all(const uint32_t (&v)[R][M], int64_t t) {
-        const int64_t lo = ly0 + t * R - K;
-        if (store_lane) {
-#pragma unroll
-            for (int r = 0; r < R; r++) store_row(v[r], lo + r);
-        }
-    }
+    // Store trip t's outputs.  Rows outside the segment (pipeline fill and the tail) get an empty
+    // descriptor (num_records 0): the stores are dropped by the range check with no branch, and the row
+    // address is clamped so no out-of-buffer pointer is ever formed.
     __device__ __forceinline__ void store_masked(const uint32_t (&v)[R][M], int64_t t) {
         const int64_t lo = ly0 + t * R - K;
-        if (store_lane) {
 #pragma unroll
-            for (int r = 0; r < R; r++)
-                if (lo + r >= seg_begin && lo + r < seg_end) store_row(v[r], lo + r);
+        for (int r = 0; r < R; r++) {
+            const bool valid = lo + r >= seg_begin && lo + r < seg_end;
+            store_row(v[r], valid ? lo + r : seg_begin, valid);
         }
     }
 };
 
-// Trips: [0, t_fill) pipeline fill (no stores, garbage levels skipped), [t_fill, first_store_trip)
-// transition, [.., t_tail) steady state (every row stored, fixed memory-op count per trip), [t_tail,
-// ntrips) masked tail.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch).
+// Trips: [0, t_fill) pipeline fill (nothing valid to store, garbage levels skipped), then the steady
+// loop.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch); trip t's outputs
+// are stored at the top of trip t+1 (below).
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 __global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const uint32_t* __restrict__ src,
                                                                           uint32_t* __restrict__ dst,
@@ -251,48 +291,48 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const u
     const int64_t ntrips = (w.nsteps + R - 1) / R;
     const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
     const int64_t first_store_trip = (2 * K + R - 1) / R;
-    int64_t t_tail = (2 * K + (w.seg_end - w.seg_begin)) / R;  // trips entirely inside the stored range
-    if (t_tail < first_store_trip) t_tail = first_store_trip;
-    if (t_tail > ntrips) t_tail = ntrips;
 
-    uint32_t nxt[R][M], v[R][M];
-    w.load(nxt, 0);
+    // Trip t (rows of trip t in `cur`, trip t-1's outputs in `other`):
+    //   [wait for all memory ops of trip t-1] [store `other`] [prefetch trip t+1 into `other`]
+    //   [compute trip t in place in `cur`]
+    // Stores are deferred by one trip so the wait at the top never covers an operation issued less than
+    // a whole trip earlier (the wait-count pass treats pending loads and stores as completing out of
+    // order: waiting for a prefetched row with a younger store in flight would drain that store too),
+    // and the two row buffers alternate roles (A/B) so no register copy or early wait joins a prefetch.
+    uint32_t A[R][M], B[R][M];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int j = 0; j < M; j++) B[r][j] = 0;
+    w.load(A, 0);
+    auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], int64_t tt, auto skip) {
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        w.store_masked(other, tt - 1);
+        w.load(other, (tt + 1) * R);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
+        w.template process<decltype(skip)::value>(cur, tt);
+    };
+    using Skip = std::true_type;
+    using NoSkip = std::false_type;
+    const int64_t fill_pairs = (t_fill < ntrips ? t_fill : ntrips) / 2;
     int64_t t = 0;
-    for (; t < t_fill; t++) {
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
-        w.load(nxt, (t + 1) * R);
-        w.template process<true>(v, t);
+    for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
+        trip(A, B, t, Skip{});
+        trip(B, A, t + 1, Skip{});
     }
-    for (; t < first_store_trip && t < ntrips; t++) {  // transition trip (when R does not divide 2K)
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
-        w.load(nxt, (t + 1) * R);
-        w.template process<true>(v, t);
-        w.store_masked(v, t);
+    for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
+        trip(A, B, t, NoSkip{});
+        trip(B, A, t + 1, NoSkip{});
     }
-    for (; t < t_tail; t++) {  // steady state
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
-        w.load(nxt, (t + 1) * R);
-        w.template process<false>(v, t);
-        w.store_all(v, t);
+    if (t < ntrips) {  // odd trip count: one more trip, outputs land in A
+        trip(A, B, t, NoSkip{});
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        w.store_masked(A, t);
+    } else {
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        w.store_masked(B, t - 1);
     }
-    for (; t < ntrips; t++) {  // masked tail
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int j = 0; j < M; j++) v[r][j] = nxt[r][j];
-        w.load(nxt, (t + 1) * R);
-        w.template process<false>(v, t);
-        w.store_masked(v, t);
-    }
+    (void)first_store_trip;
 }
 
 // ------------------------------------------------------------------------------------------------

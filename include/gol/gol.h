@@ -52,6 +52,10 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
  * The initial board is all dead. */
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
+/* As gol_create with an explicit packed layout: ilv = 0 (auto, gol_default_ilv) or 1, 2, 4 words per
+ * interleaved block (width must be a multiple of 32*ilv). */
+int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, int ilv,
+                  gol_board** out);
 int gol_destroy(gol_board* b);
 
 /* Board I/O: cells[x + y*width], len == width*height.  Replaces createCell's `alive` argument

@@ -48,7 +48,7 @@ def test_layout_choice():
     from gameoflifewithactors_amd import _lib
 
     lib = _lib.load()
-    assert [lib.gol_default_ilv(w) for w in (100, 32, 96, 64, 320, 128, 65536)] == [0, 1, 1, 2, 2, 4, 4]
+    assert [lib.gol_default_ilv(w) for w in (100, 32, 96, 64, 320, 128, 65536)] == [0, 1, 1, 2, 2, 2, 2]
     assert all(lib.gol_supported_k(lib.gol_default_tblock(m), m) for m in (1, 2, 4))
     assert lib.gol_supported_k(16, 4) == 0 and lib.gol_supported_k(32, 1) == 1
 

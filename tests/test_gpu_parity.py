@@ -32,14 +32,17 @@ def _rand(h, w, seed, p=0.5):
 
 # ---------------------------------------------------------------- small boards vs the oracle
 @pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("ilv", [1, 2, 4])
 @pytest.mark.parametrize("w,h", [(32, 3), (64, 5), (96, 64), (128, 127), (320, 77), (2048, 40), (4000 + 96, 9)])
-def test_packed_step_matches_oracle(gol, oracle, boundary, w, h):
+def test_packed_step_matches_oracle(gol, oracle, boundary, ilv, w, h):
+    if w % (32 * ilv):
+        pytest.skip("width is not a whole number of blocks for this layout")
     b0 = _rand(h, w, w * 1000 + h)
     want = {1: oracle.c_run(b0, 1, boundary)}
     want[37] = oracle.c_run(want[1], 36, boundary)
     for k in KS:
-        with gol.Board(w, h, boundary, tblock_k=k) as b:
-            assert b.info()["packed"]
+        with gol.Board(w, h, boundary, tblock_k=k, ilv=ilv) as b:
+            assert b.info()["packed"] and b.info()["ilv"] == ilv
             b.set_cells(b0)
             assert np.array_equal(b.get_cells(), b0)
             b.step(1)
@@ -60,11 +63,12 @@ def test_byte_path_matches_oracle(gol, oracle, boundary, w, h):
 
 
 @pytest.mark.parametrize("k", KS)
-def test_deep_pass_matches_oracle_many_generations(gol, oracle, k):
+@pytest.mark.parametrize("ilv", [1, 2, 4])
+def test_deep_pass_matches_oracle_many_generations(gol, oracle, k, ilv):
     """One long run (K-blocked passes + remainder passes) against 150 oracle generations."""
     b0 = _rand(96, 256, 99 + k, p=0.35)
     for boundary in (0, 1):
-        with gol.Board(256, 96, boundary, tblock_k=k) as b:
+        with gol.Board(256, 96, boundary, tblock_k=k, ilv=ilv) as b:
             b.set_cells(b0).step(150)
             assert np.array_equal(b.get_cells(), oracle.c_run(b0, 150, boundary))
 
@@ -233,18 +237,18 @@ def _splitmix_window(seed, width, xs, ys):
 
 
 def test_65536_temporal_block_invariance(gol):
-    """The same 65536^2 run at every K gives the same board (hash + population)."""
+    """The same 65536^2 run at every layout and depth gives the same board (hash + population)."""
     n = 65536
     res = {}
-    with gol.Board(n, n, tblock_k=1) as ref:
+    with gol.Board(n, n, tblock_k=1, ilv=1) as ref:
         ref.seed_splitmix(7)
         ref.step(48)
-        res[1] = (ref.hash(), ref.population())
-    for k in (8, 16, 32):
-        with gol.Board(n, n, tblock_k=k) as b:
+        res[(1, 1)] = (ref.hash(), ref.population())
+    for ilv, k in ((1, 16), (1, 32), (2, 12), (2, 16), (4, 6), (4, 8)):
+        with gol.Board(n, n, tblock_k=k, ilv=ilv) as b:
             b.seed_splitmix(7)
             b.step(48)
-            res[k] = (b.hash(), b.population())
+            res[(ilv, k)] = (b.hash(), b.population())
     assert len(set(res.values())) == 1, res
 
 
