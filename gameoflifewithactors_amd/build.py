@@ -37,15 +37,18 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tuple = ()) -> str:
-    """Compile SOURCES for gfx950 into `lib`.  `defines` (e.g. ("GOL_XLANE=0",)) build A/B variants."""
-    deps = SOURCES + HEADERS + [os.path.abspath(__file__)]
+def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tuple = (),
+          step_src: str | None = None, flags: tuple = ()) -> str:
+    """Compile SOURCES for gfx950 into `lib`.  `defines` (e.g. ("GOL_XLANE=0",)) and `step_src` (another
+    revision of gol_step.hip) build A/B variants for experiments."""
+    sources = [step_src or SOURCES[0]] + SOURCES[1:]
+    deps = sources + HEADERS + [os.path.abspath(__file__)]
     if not force and not _stale(lib, deps):
         return lib
     objs = []
-    tag = "_".join(d.replace("=", "") for d in defines)
+    tag = "_".join(d.replace("=", "") for d in defines) + ("_alt" if step_src else "") + ("_fl" if flags else "")
     procs = []
-    for src in SOURCES:  # compile the translation units in parallel (gol_step.hip dominates)
+    for src in sources:  # compile the translation units in parallel (gol_step.hip dominates)
         obj = os.path.join(CSRC, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")
         cmd = [
             _hipcc(),
@@ -58,11 +61,13 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tu
             "hip",
             "-I",
             os.path.join(ROOT, "include"),
+            "-I",
+            CSRC,
             "-c",
             src,
             "-o",
             obj,
-        ] + [f"-D{d}" for d in defines]
+        ] + [f"-D{d}" for d in defines] + list(flags)
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((subprocess.Popen(cmd), cmd))

@@ -24,7 +24,10 @@ namespace gol {
 
 static constexpr int kWave = 64;
 static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip
-static constexpr int kWavesPerBlock = 4;
+#ifndef GOL_WAVES_PER_BLOCK
+#define GOL_WAVES_PER_BLOCK 4
+#endif
+static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 
 // Cross-lane exchange of the block-edge words.  Measured on gfx950 (tools/ubench/valu_rates.hip,
 // profiles/r1/valu_rates_gfx950.jsonl): a DPP move costs a half-rate VALU issue slot; ds_bpermute_b32
@@ -36,6 +39,11 @@ static constexpr int kWavesPerBlock = 4;
 // GOL_BATCH_XLANE: issue a level's ds_bpermute exchanges for all rows of a trip before its arithmetic
 #ifndef GOL_BATCH_XLANE
 #define GOL_BATCH_XLANE 1
+#endif
+// GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
+// outputs folded into one register), 2 = no arithmetic (the pass copies the board)
+#ifndef GOL_DEBUG_MODE
+#define GOL_DEBUG_MODE 0
 #endif
 struct XLane {
     int left_addr, right_addr;  // byte addresses of lane-1 / lane+1 for ds_bpermute
@@ -186,7 +194,13 @@ struct StreamWave {
                 // step) are never used unmasked: clamp the address into the buffer
                 br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
+#if GOL_DEBUG_MODE == 1
+#pragma unroll
+            for (int j = 0; j < M; j++)
+                buf[r][j] = ((uint32_t)load_off * 0x9E3779B9u) ^ ((uint32_t)br * 0x85EBCA6Bu + (uint32_t)j);
+#else
             V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
+#endif
             if (BOUNDED) {
                 const int64_t gy = a.y0 + ly0 + first_step + r;
                 const uint32_t m = (gy >= 0 && gy < a.height) ? colmask : 0u;
@@ -217,6 +231,7 @@ struct StreamWave {
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
     template <bool SKIP>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
+        if (GOL_DEBUG_MODE == 2) return;
         const int64_t lyt = ly0 + t * R;
 #pragma unroll
         for (int g = 0; g < K; g++) {
@@ -256,7 +271,13 @@ struct StreamWave {
         }
     }
 
+    uint32_t dbg_acc = 0;
     __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
+#if GOL_DEBUG_MODE == 1
+#pragma unroll
+        for (int j = 0; j < M; j++) dbg_acc ^= v[j];
+        return;
+#endif
         V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? row_bytes : 0), store_off, v);
     }
     // Store trip t's outputs.  Rows outside the segment (pipeline fill and the tail) get an empty
@@ -275,8 +296,19 @@ struct StreamWave {
 // Trips: [0, t_fill) pipeline fill (nothing valid to store, garbage levels skipped), then the steady
 // loop.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch); trip t's outputs
 // are stored at the top of trip t+1 (below).
+// Minimum waves per SIMD the register allocator must fit (0 = compiler's choice), per depth and layout.
+template <int K, int M>
+struct MinWaves {
+#ifdef GOL_MIN_WAVES
+    static constexpr int value = (5 * K * M <= 96) ? 4 : (5 * K * M <= 130 ? 3 : (5 * K * M <= 200 ? 2 : 1));
+#else
+    static constexpr int value = 1;
+#endif
+};
+
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
-__global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const uint32_t* __restrict__ src,
+__global__ __launch_bounds__(kWave* kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(MinWaves<K, M>::value)))
+void gol_stream_step(const uint32_t* __restrict__ src,
                                                                           uint32_t* __restrict__ dst,
                                                                           StreamArgs a) {
     using W = StreamWave<K, M, BOUNDED, WRAP_ROWS>;
@@ -333,6 +365,9 @@ __global__ __launch_bounds__(kWave* kWavesPerBlock) void gol_stream_step(const u
         w.store_masked(B, t - 1);
     }
     (void)first_store_trip;
+#if GOL_DEBUG_MODE == 1
+    if (w.dbg_acc == 0x5EED1234u) dst[lane] = w.dbg_acc;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
