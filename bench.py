@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU actor baseline sample length")
     p.add_argument("--cpu-board", type=int, default=512, help="CPU actor baseline board side")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="N > 1: nccl (= RCCL over xGMI, the product path) or gloo (host-staged halo; lets "
+                   "several ranks share one GPU in rehearsals)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -100,7 +103,10 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from gameoflifewithactors_amd import TORUS, BOUNDED
     from gameoflifewithactors_amd.strips import StripRunner
@@ -137,7 +143,8 @@ def main():
     dt = time.perf_counter() - t0
     kernel_s = ev0.elapsed_time(ev1) / 1e3  # HIP events on the stream the step kernels run on
     if world > 1:
-        t = torch.tensor([dt, kernel_s], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt, kernel_s], device="cuda" if args.dist_backend == "nccl" else "cpu",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kernel_s = float(t[0]), float(t[1])
 
@@ -150,7 +157,8 @@ def main():
     alg_bytes = 2 * cells_gpu / 8  # read + write the packed strip once per pass
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     valu_tops = OPS_PER_WORD_GEN * (cells_gpu / 32) * k / avg_launch_s / 1e12
-    traffic = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}")
+    tr = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}") or {}
+    traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)
 
     result = None
     if rank == 0:
@@ -185,6 +193,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": "profiles/pmc_traffic.json (tools/pmc_traffic.sh)" if traffic else None,
                 "kernel": f"gol_stream_step<K={k}, M={ilv}>",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),

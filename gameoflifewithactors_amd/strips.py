@@ -219,6 +219,8 @@ class StripRunner:
         if self.device.type == "cuda":
             self.compute_stream.synchronize()
         if self.world > 1:
+            if acc.is_cuda and dist.get_backend(self.group) == "gloo":
+                acc = acc.cpu()  # gloo reduces host tensors
             dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
         return int(acc.item()) & 0xFFFFFFFFFFFFFFFF
 
@@ -238,6 +240,8 @@ class DistExchange:
         self.group = group
 
     def post(self, r: "StripRunner", buf: torch.Tensor, k: int):
+        if buf.is_cuda and dist.get_backend(self.group) == "gloo":
+            return self._post_staged(r, buf, k)
         g, h = r.geom.ghost, r.geom.rows
         ops = []
         if r.up is not None:  # my top rows -> up's bottom ghost
@@ -249,6 +253,30 @@ class DistExchange:
         if r.up is not None:
             ops.append(dist.P2POp(dist.irecv, buf[g - k:g], r.up, self.group, tag=2))
         return dist.batch_isend_irecv(ops) if ops else []
+
+    def _post_staged(self, r: "StripRunner", buf: torch.Tensor, k: int):
+        """gloo moves host tensors only: stage the edge rows through host memory, synchronously (no
+        overlap).  Lets the GPU strip path run over gloo, e.g. several ranks sharing one GPU in tests;
+        the multi-GPU bench uses NCCL (RCCL), which sends device memory directly."""
+        g, h = r.geom.ghost, r.geom.rows
+        ops, recvs = [], []
+        if r.up is not None:
+            ops.append(dist.P2POp(dist.isend, buf[g:g + k].cpu(), r.up, self.group, tag=1))
+        if r.down is not None:
+            ops.append(dist.P2POp(dist.isend, buf[g + h - k:g + h].cpu(), r.down, self.group, tag=2))
+        if r.down is not None:
+            t = torch.empty((k, buf.shape[1]), dtype=buf.dtype)
+            ops.append(dist.P2POp(dist.irecv, t, r.down, self.group, tag=1))
+            recvs.append((g + h, t))
+        if r.up is not None:
+            t = torch.empty((k, buf.shape[1]), dtype=buf.dtype)
+            ops.append(dist.P2POp(dist.irecv, t, r.up, self.group, tag=2))
+            recvs.append((g - k, t))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for row, t in recvs:
+            buf[row:row + k].copy_(t)
+        return []
 
 
 class LocalExchange:

@@ -51,3 +51,75 @@ def test_strip_runner_single_rank_matches_board():
         with Board(4096, 1000, boundary, tblock_k=8) as b:
             b.seed_splitmix(5).step(100)
             assert r.hash() == b.hash() and r.population() == b.population()
+
+
+def _dist_worker(rank, world, port, width, height, boundary, k, gens, seed, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = None
+    try:
+        from gameoflifewithactors_amd.strips import StripRunner
+
+        torch.cuda.set_device(0)
+        r = StripRunner(width, height, boundary, k, rank=rank, world=world, device=torch.device("cuda", 0))
+        r.seed_splitmix(seed)
+        r.step(gens)
+        res = (rank, r.hash(), r.population(), r.generation)
+    finally:
+        q.put(res if res is not None else (rank, None, None, None))
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,boundary,k", [(2, 0, 12), (3, 1, 8)])
+def test_multiprocess_strips_match_single_board(world, boundary, k):
+    """The bench's N > 1 path -- one process per strip, StripRunner + HipEngine + DistExchange -- with the
+    ranks sharing this one GPU over gloo (host-staged halo; RCCL needs one GPU per rank).  Every rank's
+    allreduced hash must equal the single-board run."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from gameoflifewithactors_amd import Board
+
+    width, height, gens, seed = 4096, 600, 50, 31
+    with Board(width, height, boundary, tblock_k=k) as b:
+        b.seed_splitmix(seed).step(gens)
+        want = (b.hash(), b.population())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, width, height, boundary, k, gens, seed, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(r[1] is not None for r in res), res
+    assert all((r[1], r[2]) == want for r in res), (res, want)
+    assert all(r[3] == gens for r in res)
+
+
+def test_bench_two_ranks_over_gloo():
+    """bench.py --gpus 2 end to end (torchrun, two ranks on this GPU, gloo halo): one JSON line."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29613", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--height", "4096", "--dist-backend", "gloo", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["value"] > 0 and r["config"]["height"] == 2 * 4096
