@@ -101,10 +101,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torchrun")
-    torch.cuda.set_device(local)
+    # one GPU per rank; a gloo rehearsal may place several ranks on one GPU
+    dev = local if args.dist_backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
 
@@ -118,7 +120,7 @@ def main():
     lib = _lib.load()
     ilv = lib.gol_default_ilv(W)
     k = args.tblock or lib.gol_default_tblock(ilv)
-    runner = StripRunner(W, H, boundary, k, rank=rank, world=world, device=torch.device("cuda", local))
+    runner = StripRunner(W, H, boundary, k, rank=rank, world=world, device=torch.device("cuda", dev))
     runner.seed_splitmix(args.seed)
 
     for _ in range(args.warmup):

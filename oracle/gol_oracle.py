@@ -263,6 +263,11 @@ def c_oracle() -> ctypes.CDLL:
         lib.dn_random_next.restype = ctypes.c_int32
         lib.dn_random_next_max.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         lib.dn_random_next_max.restype = ctypes.c_int32
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        lib.fast_run.argtypes = [u64p, i64, i64, ctypes.c_int, i64, ctypes.c_int, i64, u64p,
+                                 ctypes.POINTER(ctypes.c_int64)]
+        lib.fast_hash.argtypes = [u64p, i64, i64]
+        lib.fast_hash.restype = ctypes.c_uint64
         _C = lib
     return _C
 
@@ -297,3 +302,36 @@ def c_seed_splitmix(width: int, height: int, seed: int) -> np.ndarray:
     b = np.zeros((height, width), dtype=np.uint8)
     c_oracle().oracle_seed_splitmix(_p(b), width, height, seed)
     return b
+
+
+# ---------------------------------------------------------------- bit-packed long runs (gol_fast.c)
+def pack64(b: np.ndarray) -> np.ndarray:
+    """(H, W) uint8 cells -> (H, W/64) uint64, bit i of word j = cell 64j + i (W % 64 == 0)."""
+    h, w = b.shape
+    if w % 64:
+        raise ValueError("pack64 needs W % 64 == 0")
+    return np.packbits(np.ascontiguousarray(b, dtype=np.uint8), axis=1, bitorder="little").view("<u8").copy()
+
+
+def unpack64(words: np.ndarray, width: int) -> np.ndarray:
+    return np.unpackbits(words.view(np.uint8), axis=1, bitorder="little")[:, :width].astype(np.uint8)
+
+
+def fast_run(b: np.ndarray, generations: int, boundary: int = TORUS, threads: int | None = None,
+             every: int = 0):
+    """gol_fast.c: run a W % 64 == 0 board `generations` steps on `threads` host threads.  Returns
+    (final board (H, W) uint8, [(generation, hash, population)] every `every` generations)."""
+    lib = c_oracle()
+    h, w = b.shape
+    words = pack64(b)
+    n = generations // every if every > 0 else 0
+    hashes = np.zeros(max(n, 1), np.uint64)
+    pops = np.zeros(max(n, 1), np.int64)
+    rc = lib.fast_run(words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), w, h, boundary, generations,
+                      threads or (os.cpu_count() or 1), every,
+                      hashes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                      pops.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    if rc:
+        raise ValueError("fast_run rejected the board")
+    marks = [((i + 1) * every, int(hashes[i]), int(pops[i])) for i in range(n)]
+    return unpack64(words, w), marks

@@ -269,3 +269,34 @@ def test_driver_update_view_matches_oracle(gol, oracle):
     with driver.run(seed=42, agent=fast, emit="pixels") as game:
         game.update_view()
     assert np.array_equal(frames[-1], frames[0])
+
+
+# ---------------------------------------------------------------- long runs (BASELINE.json configs 2 and 5)
+def _golden_long():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_long.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["c2_4096_torus_dotnet42", "c5_gun_rpent_4096_torus", "c5_gun_rpent_256_bounded"])
+@pytest.mark.parametrize("tblock", [0, 1])
+def test_long_run_checkpoints(gol, oracle, name, tblock):
+    """Every checkpoint (hash + population) of the long-run fixtures -- 4096^2 x 10k generations seeded
+    by .NET Random (config 2), Gosper gun + R-pentomino x 100k generations on a 4096^2 torus and the
+    256^2 bounded board (config 5) -- at the engine's default temporal block and at k = 1."""
+    case = _golden_long()[name]
+    with gol.Board(case["width"], case["height"], case["boundary"], tblock_k=tblock) as b:
+        if case["init"] == "dotnet-mod2":
+            b.seed_dotnet(case["seed"], gol.INIT_DOTNET_MOD2)
+        else:
+            for pat, x, y in case["patterns"]:
+                b.place_rle(getattr(oracle, pat), x, y)
+        assert b.hash() == case["initial_hash"]
+        done = 0
+        for gen, h, pop in case["checkpoints"]:
+            b.step(gen - done)
+            done = gen
+            assert (b.hash(), b.population()) == (h, pop), (name, gen)
+        assert b.generation == case["generations"]

@@ -187,3 +187,61 @@ def test_rle_parser(oracle):
         [(1, 0), (2, 1), (0, 2), (1, 2), (2, 2)]
     )
     assert len(oracle.parse_rle(oracle.GOSPER_GUN)) == 36
+
+
+# ---------------------------------------------------------------- bit-packed long-run oracle (gol_fast.c)
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h,threads", [(64, 3, 1), (128, 77, 3), (192, 64, 8), (256, 5, 2)])
+def test_fast_oracle_matches_byte_oracle(oracle, boundary, w, h, threads):
+    b = (np.random.default_rng(w * h + boundary).random((h, w)) < 0.4).astype(np.uint8)
+    got, marks = oracle.fast_run(b, 37, boundary, threads=threads, every=5)
+    assert np.array_equal(got, oracle.c_run(b, 37, boundary))
+    assert [m[0] for m in marks] == [5, 10, 15, 20, 25, 30, 35]
+    mid = oracle.c_run(b, 20, boundary)
+    assert marks[3][1:] == (oracle.board_hash(mid), oracle.population(mid))
+
+
+def test_fast_oracle_known_answers(oracle):
+    b = np.zeros((1024, 1024), np.uint8)
+    oracle.place_rle(b, oracle.R_PENTOMINO, 511, 511)
+    got, _ = oracle.fast_run(b, 1103, oracle.BOUNDED)
+    assert oracle.population(got) == 116
+    g = np.zeros((64, 64), np.uint8)
+    oracle.place_rle(g, oracle.GLIDER, 3, 7)
+    assert np.array_equal(oracle.fast_run(g, 4 * 64)[0], g)
+
+
+def _golden_long():
+    import json
+
+    p = os.path.join(os.path.dirname(__file__), "golden", "golden_long.json")
+    with open(p) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name,gens", [("c2_4096_torus_dotnet42", 100), ("c5_gun_rpent_256_bounded", 2000),
+                                       ("c5_gun_rpent_4096_torus", 500)])
+def test_long_golden_first_checkpoints_from_byte_oracle(oracle, name, gens):
+    """Pin the long-run fixtures' leading checkpoints with the independent byte-per-cell oracle."""
+    case = _golden_long()[name]
+    if case["init"] == "dotnet-mod2":
+        b = oracle.c_seed_dotnet(case["width"], case["height"], case["seed"], 0)
+    else:
+        b = np.zeros((case["height"], case["width"]), np.uint8)
+        for pat, x, y in case["patterns"]:
+            oracle.place_rle(b, getattr(oracle, pat), x, y)
+    assert oracle.c_hash(b) == case["initial_hash"]
+    if case["width"] == 4096 and case["init"] == "patterns":
+        # Exact by the light cone: each pattern sits >= gens + 8 cells from the board edges and from the
+        # other pattern's cone, so a bounded byte-oracle run on each cone window equals the torus run there
+        # and every cell outside both windows stays dead.
+        want = np.zeros_like(b)
+        for pat, x, y in case["patterns"]:
+            x0, y0, x1, y1 = x - gens - 8, y - gens - 8, x + 40 + gens + 8, y + 40 + gens + 8
+            assert 0 <= x0 and 0 <= y0 and x1 <= case["width"] and y1 <= case["height"]
+            assert not want[y0:y1, x0:x1].any()
+            want[y0:y1, x0:x1] = oracle.c_run(b[y0:y1, x0:x1], gens, oracle.BOUNDED)
+    else:
+        want = oracle.c_run(b, gens, case["boundary"])
+    mark = [m for m in case["checkpoints"] if m[0] == gens][0]
+    assert (mark[1], mark[2]) == (oracle.board_hash(want), oracle.population(want))
