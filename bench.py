@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--width", type=int, default=65536)
     p.add_argument("--height", type=int, default=65536, help="rows per GPU (board height = height * gpus)")
+    p.add_argument("--board", type=int, default=0,
+                   help="strong scaling: a fixed board x board torus split over the GPUs (BASELINE config 4: "
+                   "262144); overrides --width/--height")
     p.add_argument("--tblock", type=int, default=0,
                    help="generations per pass (0 = the engine's default for the board layout)")
     p.add_argument("--seed", type=int, default=0x5EED)
@@ -116,7 +119,11 @@ def main():
     from gameoflifewithactors_amd import _lib
 
     boundary = TORUS if args.boundary == "torus" else BOUNDED
-    W, H = args.width, args.height * world
+    if args.board:
+        args.width, args.height = args.board, args.board // world  # rows per GPU (last rank may own more)
+        W, H = args.board, args.board
+    else:
+        W, H = args.width, args.height * world
     lib = _lib.load()
     ilv = lib.gol_default_ilv(W)
     k = args.tblock or lib.gol_default_tblock(ilv)
@@ -173,7 +180,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.board else "weak",
             "vs_baseline": None,
             "dtype": "u32 (bit-packed cells)",
             "data": "synthetic (splitmix 50% fill generated on device)",

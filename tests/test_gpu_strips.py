@@ -123,3 +123,24 @@ def test_bench_two_ranks_over_gloo():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["config"]["height"] == 2 * 4096
+
+
+def test_262144_board_strips_match_single_board():
+    """BASELINE.json config 4 geometry: a 262144^2 torus (8 GiB per packed buffer, 2^31 words -- 64-bit
+    indexing) as one board and as 8 row strips of 32768 rows (the 8-GPU partition, here in one process),
+    same hash and population after 24 generations."""
+    from gameoflifewithactors_amd import Board
+    from gameoflifewithactors_amd.strips import LocalBoard
+
+    n, gens, seed = 262144, 24, 0xC4
+    with Board(n, n, tblock_k=12) as b:
+        b.seed_splitmix(seed).step(gens)
+        want = (b.hash(), b.population())
+    torch.cuda.empty_cache()
+    lb = LocalBoard(n, n, 0, 12, 8)
+    lb.seed_splitmix(seed)
+    lb.step(gens)
+    got_hash = lb.hash()
+    del lb
+    torch.cuda.empty_cache()
+    assert got_hash == want[0]
