@@ -40,6 +40,14 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 #ifndef GOL_BATCH_XLANE
 #define GOL_BATCH_XLANE 1
 #endif
+// GOL_EARLY_XLANE: issue level g+1's right-hand exchange (ds_bpermute) as soon as level g has produced the
+// row, pinned there by a scheduling barrier that only DS instructions may not cross, so the LDS-pipe
+// latency overlaps the rest of level g instead of stalling level g+1
+#ifndef GOL_EARLY_XLANE
+#define GOL_EARLY_XLANE 0
+#endif
+// sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
+static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
 // GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
 // outputs folded into one register), 2 = no arithmetic (the pass copies the board)
 #ifndef GOL_DEBUG_MODE
@@ -233,9 +241,15 @@ struct StreamWave {
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
         if (GOL_DEBUG_MODE == 2) return;
         const int64_t lyt = ly0 + t * R;
+#if GOL_EARLY_XLANE
+        uint32_t right[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) right[r] = xl.from_right(v[r][0]);
+#endif
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
+#if !GOL_EARLY_XLANE
             // block-edge words of the right-hand lanes for all R rows first: the LDS-pipe exchanges
             // (ds_bpermute) then overlap each other and the arithmetic below instead of each stalling
             // its own row; the DPP (VALU) moves from the left stay next to their use
@@ -243,6 +257,7 @@ struct StreamWave {
 #if GOL_BATCH_XLANE
 #pragma unroll
             for (int r = 0; r < R; r++) right[r] = xl.from_right(v[r][0]);
+#endif
 #endif
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
@@ -254,7 +269,7 @@ struct StreamWave {
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-#if !GOL_BATCH_XLANE
+#if !GOL_BATCH_XLANE && !GOL_EARLY_XLANE
                 right[r] = xl.from_right(v[r][0]);
                 right[r + 1] = xl.from_right(v[r + 1][0]);
 #endif
@@ -267,7 +282,17 @@ struct StreamWave {
                     v[r][j] = o0[j];
                     v[r + 1][j] = o1[j];
                 }
+#if GOL_EARLY_XLANE
+                if (g + 1 < K) {
+                    right[r] = xl.from_right(o0[0]);
+                    right[r + 1] = xl.from_right(o1[0]);
+                    __builtin_amdgcn_sched_barrier(kAllButDs);
+                }
+#endif
             }
+#if GOL_EARLY_XLANE == 2
+            __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges
+#endif
         }
     }
 

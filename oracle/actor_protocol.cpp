@@ -25,8 +25,16 @@
 // test suite checks that equality.  A generation ends when the update agent has rendered the frame
 // (its Dictionary reached gridProduct entries).
 //
-// Usage: actor_protocol W H GENS THREADS SEED [MIN_SECONDS] [INIT]
+// Without the barrier (SURVEY.md section 8f, rank 4 -- demonstration only, never a parity reference):
+// SCHEDULE "racy-seq:S" replays one schedule the reference permits, deterministically on one thread:
+// the driver posts Reset to the cells in a shuffled order (seed S), and every message that Reset causes
+// is delivered before the next Reset is posted.  A State request then reaches the cells not yet reset in
+// this generation, which answer with their stale wasAlive (GameOfLifeLogic.fs:54 reads wasAlive, set only
+// by Reset, L52) -- the reference's race, made reproducible.  Different S give different boards.
+//
+// Usage: actor_protocol W H GENS THREADS SEED [MIN_SECONDS] [INIT] [SCHEDULE]
 //   INIT = "dotnet-mod2" (default; GameOfLifeDriver.fs:9-11) or "splitmix"
+//   SCHEDULE = "barrier" (default) or "racy-seq:S"
 //   Runs GENS generations, or as many as needed to reach MIN_SECONDS of wall time when GENS <= 0.
 //   Prints one JSON line: generations, seconds, cell_updates_per_s, messages, hash, population.
 #include <atomic>
@@ -78,7 +86,8 @@ struct CellState {  // GameOfLifeLogic.fs:24-30 `State` + the per-cell Dictionar
 class System {
    public:
     System(int64_t W, int64_t H, int threads, const uint8_t* init)
-        : W_(W), H_(H), n_(W * H), actors_(n_ + 1), cells_(n_), queues_(threads), nthreads_(threads) {
+        : W_(W), H_(H), n_(W * H), actors_(n_ + 1), cells_(n_), queues_(threads > 0 ? threads : 1),
+          nthreads_(threads) {
         agent_id_ = (int32_t)n_;
         for (int64_t x = 0; x < W; x++)
             for (int64_t y = 0; y < H; y++) {
@@ -127,6 +136,20 @@ class System {
         done_cv_.wait(lk, [this] { return frame_done_.load() && acks_ == nthreads_; });
     }
 
+    // One generation without the phase barrier, on the calling thread (construct with threads = 0):
+    // Reset to the cells in the order `perm`, each Reset's message cascade delivered before the next.
+    void generation_racy_sequential(const std::vector<int32_t>& perm) {
+        uint64_t local = 0;
+        frame_done_ = false;
+        post(agent_id_, Msg{kViewReset, 0, -1}, 0);
+        drain(local);
+        for (int32_t id : perm) {
+            post(id, Msg{kReset, 0, -1}, 0);
+            drain(local);
+        }
+        messages_.fetch_add(local);
+    }
+
     void snapshot(uint8_t* out) const {
         for (int64_t y = 0; y < H_; y++)
             for (int64_t x = 0; x < W_; x++) out[x + y * W_] = pixels_[x + y * W_] ? 1 : 0;
@@ -154,6 +177,11 @@ class System {
     };
 
     void enqueue_raw(int32_t to, const Msg& m) { actors_[to].box.push_back(m); }
+
+    void drain(uint64_t& nmsg) {
+        int32_t id;
+        while (queues_[0].pop(id)) run_actor(id, 0, nmsg);
+    }
 
     void post(int32_t to, const Msg& m, int self_q) {
         Actor& a = actors_[to];
@@ -318,10 +346,20 @@ int main(int argc, char** argv) {
     long long seed = std::atoll(argv[5]);
     double min_s = argc > 6 ? std::atof(argv[6]) : 0.0;
     std::string init = argc > 7 ? argv[7] : "dotnet-mod2";
-    if (W < 3 || H < 3 || threads < 1) {
-        std::fprintf(stderr, "W, H must be >= 3 and THREADS >= 1\n");
+    std::string schedule = argc > 8 ? argv[8] : "barrier";
+    const bool racy = schedule.rfind("racy-seq:", 0) == 0;
+    if (W < 3 || H < 3 || threads < 1 || (!racy && schedule != "barrier")) {
+        std::fprintf(stderr, "W, H must be >= 3, THREADS >= 1, SCHEDULE barrier | racy-seq:S\n");
         return 2;
     }
+    uint64_t rs = racy ? std::strtoull(schedule.c_str() + 9, nullptr, 10) : 0;
+    auto next_rand = [&rs]() {  // splitmix64 stream for the schedule shuffle
+        uint64_t z = (rs += 0x9E3779B97F4A7C15ULL);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    if (racy) threads = 0;
     std::vector<uint8_t> board((size_t)(W * H));
     if (init == "splitmix")
         oracle_seed_splitmix(board.data(), W, H, (uint64_t)seed);
@@ -335,15 +373,22 @@ int main(int argc, char** argv) {
     for (;;) {
         if (gens > 0 && done >= gens) break;
         if (gens <= 0 && secs >= min_s && done > 0) break;
-        sys.generation();
+        if (racy) {
+            std::vector<int32_t> perm((size_t)(W * H));
+            for (size_t i = 0; i < perm.size(); i++) perm[i] = (int32_t)i;
+            for (size_t i = perm.size() - 1; i > 0; i--) std::swap(perm[i], perm[next_rand() % (i + 1)]);
+            sys.generation_racy_sequential(perm);
+        } else {
+            sys.generation();
+        }
         done++;
         secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     sys.snapshot(board.data());
     std::printf(
-        "{\"width\": %lld, \"height\": %lld, \"generations\": %lld, \"threads\": %d, \"seconds\": %.6f, "
+        "{\"schedule\": \"%s\", \"width\": %lld, \"height\": %lld, \"generations\": %lld, \"threads\": %d, \"seconds\": %.6f, "
         "\"cell_updates_per_s\": %.3f, \"messages\": %llu, \"hash\": %llu, \"population\": %lld}\n",
-        (long long)W, (long long)H, (long long)done, threads, secs, (double)(W * H) * done / secs,
+        schedule.c_str(), (long long)W, (long long)H, (long long)done, threads, secs, (double)(W * H) * done / secs,
         (unsigned long long)sys.messages(), (unsigned long long)oracle_hash(board.data(), W, H),
         (long long)oracle_population(board.data(), W, H));
     return 0;

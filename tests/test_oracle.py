@@ -135,6 +135,27 @@ def test_actor_protocol_equals_synchronous_oracle_c1(oracle, seed):
     assert r["messages"] == 100 * (18 * 100 * 100 + 1)  # 18 messages per cell per generation + view reset
 
 
+def test_actor_protocol_without_barrier_is_schedule_dependent(oracle):
+    """without the Reset->State phase barrier the reference protocol is racy.  The
+    deterministic racy schedule (racy-seq:S) reproduces it: a fixed schedule seed gives a fixed board,
+    different seeds give different boards, and none equals the synchronous step -- which is why parity
+    is defined under the barrier."""
+    exe = os.path.join(ROOT, "oracle", "build", "actor_protocol")
+
+    def run(schedule):
+        out = subprocess.run([exe, "12", "12", "6", "1", "42", "0", "dotnet-mod2", schedule], check=True,
+                             capture_output=True, text=True).stdout
+        return json.loads(out)
+
+    sync = oracle.c_run(oracle.seed_dotnet(12, 12, 42, 0), 6, 0)
+    assert run("barrier")["hash"] == oracle.c_hash(sync)
+    racy = [run(f"racy-seq:{s}") for s in (1, 2, 3)]
+    assert run("racy-seq:1")["hash"] == racy[0]["hash"]  # reproducible
+    assert len({r["hash"] for r in racy}) == 3
+    assert all(r["hash"] != oracle.c_hash(sync) for r in racy)
+    assert all(r["messages"] == 6 * (18 * 144 + 1) for r in racy)  # same 18 messages per cell per generation
+
+
 def test_actor_protocol_ragged_board(oracle):
     r = _actor(37, 23, 40, 8, 0x5EED, "splitmix")
     b = oracle.c_run(oracle.seed_splitmix(37, 23, 0x5EED), 40, 0)
