@@ -27,8 +27,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz (int32 lane-ops)
-OPS_PER_WORD_GEN = 13  # gol_bitlogic.h: 2 DPP + 2 alignbit + 9 bitop3 per 32 cells per generation
+# VALU issue peak: 256 CUs x 4 SIMDs, each retiring one full-rate wave64 instruction per 2 cycles (32
+# lane-slots per cycle) at 2.4 GHz.
+VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def valu_slots_per_word_gen(ilv: int) -> float:
+    """Algorithmic VALU issue slots per 32-cell word per generation (gol_bitlogic.h, gol_step.hip): 9
+    full-rate v_bitop3_b32 per word, plus per block of `ilv` words 2 v_alignbit_b32 and 1 DPP move, which
+    are half-rate on gfx950 (2 slots each; profiles/r1/valu_rates_gfx950.jsonl).  The block's second
+    cross-lane move is a ds_bpermute on the LDS pipe (no VALU slot)."""
+    return 9 + 6 / ilv
 
 
 def parse():
@@ -165,7 +174,8 @@ def main():
     avg_launch_s = runner.kernel_time_per_pass(kernel_s, args.steps)
     alg_bytes = 2 * cells_gpu / 8  # read + write the packed strip once per pass
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
-    valu_tops = OPS_PER_WORD_GEN * (cells_gpu / 32) * k / avg_launch_s / 1e12
+    slots = valu_slots_per_word_gen(ilv)
+    valu_tslots = slots * (cells_gpu / 32) * k / avg_launch_s / 1e12
     tr = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}") or {}
     traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)
 
@@ -209,11 +219,11 @@ def main():
             },
             "roofline_valu": {
                 "bound": "valu",
-                "achieved": round(valu_tops, 3),
-                "peak": round(VALU_PEAK_TOPS, 2),
-                "unit": "Tops/s (int32 lane-ops)",
-                "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
-                "ops_per_word_gen": OPS_PER_WORD_GEN,
+                "achieved": round(valu_tslots, 3),
+                "peak": round(VALU_PEAK_TSLOTS, 2),
+                "unit": "T lane-slots/s (VALU issue; half-rate ops count 2)",
+                "frac": round(valu_tslots / VALU_PEAK_TSLOTS, 4),
+                "slots_per_word_gen": slots,
             },
             "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
         }

@@ -123,7 +123,7 @@ bool valid_k(int k) {
 }
 
 // Interleave for a packed board of this width (gol_layout.h).  Measured on MI355X at 65536^2
-// (profiles/r1/sweep_ilv.log): ilv 2 with K = 12 is the fastest configuration, ilv 4 needs 240 window
+// (profiles/r1/sweep_ilv.log, ab_fence2.log): ilv 2 with K = 16 is the fastest configuration, ilv 4 needs 240 window
 // VGPRs at K = 8 (2 waves/SIMD) and wastes 1/9 of its lanes on a 65536-wide row, ilv 1 pays 4x the
 // funnel shifts.  GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
 int pick_ilv(int64_t width) {
@@ -137,7 +137,7 @@ int pick_ilv(int64_t width) {
 }
 
 // Default generations per pass for a layout (measured on MI355X, DESIGN.md "Temporal block depth").
-int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 24); }
+int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 16 : 32); }
 
 }  // namespace
 

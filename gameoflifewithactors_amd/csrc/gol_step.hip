@@ -24,8 +24,10 @@ namespace gol {
 
 static constexpr int kWave = 64;
 static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip
+// 8 waves per workgroup: the deep passes run 2-3 waves per SIMD, so a workgroup spans the CU's SIMDs
+// twice (profiles/r1/ab_fence2.log: +3-6 % at K = 16 / 32 over 4-wave workgroups)
 #ifndef GOL_WAVES_PER_BLOCK
-#define GOL_WAVES_PER_BLOCK 4
+#define GOL_WAVES_PER_BLOCK 8
 #endif
 static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 
@@ -40,14 +42,25 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 #ifndef GOL_BATCH_XLANE
 #define GOL_BATCH_XLANE 1
 #endif
-// GOL_EARLY_XLANE: issue level g+1's right-hand exchange (ds_bpermute) as soon as level g has produced the
-// row, pinned there by a scheduling barrier that only DS instructions may not cross, so the LDS-pipe
-// latency overlaps the rest of level g instead of stalling level g+1
+// GOL_EARLY_XLANE: 1 = issue level g+1's right-hand exchange (ds_bpermute) as soon as level g has produced
+// the row, pinned there by a scheduling barrier that only DS instructions may not cross; 2 = the same plus
+// a full scheduling barrier between levels.  Without the level barrier the scheduler interleaves levels
+// and the live register set grows past the occupancy steps (K=16, M=2: 256 VGPRs, 1 wave/SIMD; with it
+// 213 VGPRs, 2 waves/SIMD): profiles/r1/ab_early.log, ab_fence2.log.
 #ifndef GOL_EARLY_XLANE
-#define GOL_EARLY_XLANE 0
+#define GOL_EARLY_XLANE 2
+#endif
+// GOL_LEVEL_FENCE: a scheduling barrier between generation levels (keeps the scheduler from interleaving
+// levels, which inflates the live register set)
+#ifndef GOL_LEVEL_FENCE
+#define GOL_LEVEL_FENCE 0
+#endif
+// GOL_PAIR_FENCE: a scheduling barrier after every row pair (strict row-pair order inside a level)
+#ifndef GOL_PAIR_FENCE
+#define GOL_PAIR_FENCE 0
 #endif
 // sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
-static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
+[[maybe_unused]] static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
 // GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
 // outputs folded into one register), 2 = no arithmetic (the pass copies the board)
 #ifndef GOL_DEBUG_MODE
@@ -289,8 +302,11 @@ struct StreamWave {
                     __builtin_amdgcn_sched_barrier(kAllButDs);
                 }
 #endif
+#if GOL_PAIR_FENCE
+                __builtin_amdgcn_sched_barrier(0);
+#endif
             }
-#if GOL_EARLY_XLANE == 2
+#if GOL_EARLY_XLANE == 2 || GOL_LEVEL_FENCE
             __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges
 #endif
         }

@@ -7,8 +7,9 @@ rows above and below.  One pass advances k generations:
 
     1. send my top k owned rows to rank r-1 and my bottom k rows to rank r+1, receive their edge rows
        into my ghost rows (torch.distributed point-to-point: NCCL = RCCL over xGMI on GPUs, gloo on CPU)
-    2. meanwhile compute the interior rows [k, rows-k), which need no ghost rows
-    3. wait for the exchange, then compute the boundary rows [0, k) and [rows-k, rows)
+    2. meanwhile compute the interior rows [k, rows-k), which need no ghost rows (compute stream)
+    3. on a second stream, wait for the exchange only, then compute the boundary rows [0, k) and
+       [rows-k, rows): they run as soon as the ghost rows land, in the tail of the interior launch
 
 Torus: ring neighbours (r +- 1) mod N.  Bounded: the end strips have no outer neighbour; rows beyond
 the board are dead at every generation (the kernel masks them).  With N = 1 the single strip uses the
@@ -82,8 +83,12 @@ class HipEngine:
                 return k
         return 1
 
-    def alloc(self, geom: Geometry) -> torch.Tensor:
-        return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32, device=self.device)
+    def alloc(self, geom: Geometry, stream) -> torch.Tensor:
+        """A zeroed strip buffer, allocated and cleared ON `stream` (the strip's compute stream): the
+        caching allocator ties a block to the stream it was allocated on, and a fill on the default stream
+        would race with the non-blocking compute stream's first kernels."""
+        with torch.cuda.stream(stream):
+            return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32, device=self.device)
 
     def step(self, geom: Geometry, src: torch.Tensor, dst: torch.Tensor, k: int, out_begin: int, out_end: int,
              stream: torch.cuda.Stream) -> None:
@@ -97,28 +102,29 @@ class HipEngine:
                                                stream.cuda_stream), "gol_strip_seed_splitmix")
 
     def reduce(self, geom: Geometry, buf: torch.Tensor, what: str, stream) -> torch.Tensor:
-        acc = torch.zeros(1, dtype=torch.int64, device=self.device)
         s = geom.strip()
         fn = self.lib.gol_strip_hash_partial if what == "hash" else self.lib.gol_strip_population
-        with torch.cuda.stream(stream):
-            acc.zero_()
+        with torch.cuda.stream(stream):  # allocate, clear and accumulate on the strip's stream
+            acc = torch.zeros(1, dtype=torch.int64, device=self.device)
             check(fn(ctypes.byref(s), buf.data_ptr(), acc.data_ptr(), stream.cuda_stream), what)
         return acc
 
     def set_cells(self, geom: Geometry, buf: torch.Tensor, cells_u8: torch.Tensor, stream) -> None:
         s = geom.strip()
-        dev = cells_u8.to(self.device).contiguous()
-        check(self.lib.gol_strip_pack(ctypes.byref(s), dev.data_ptr(), buf.data_ptr(), stream.cuda_stream),
-              "gol_strip_pack")
+        with torch.cuda.stream(stream):
+            dev = cells_u8.to(self.device).contiguous()
+            check(self.lib.gol_strip_pack(ctypes.byref(s), dev.data_ptr(), buf.data_ptr(), stream.cuda_stream),
+                  "gol_strip_pack")
         stream.synchronize()
 
     def get_cells(self, geom: Geometry, buf: torch.Tensor, stream) -> torch.Tensor:
-        out = torch.empty((geom.rows, geom.width), dtype=torch.uint8, device=self.device)
         s = geom.strip()
-        check(self.lib.gol_strip_unpack(ctypes.byref(s), buf.data_ptr(), out.data_ptr(), geom.width, 1,
-                                        stream.cuda_stream), "gol_strip_unpack")
-        stream.synchronize()
-        return out.cpu()
+        with torch.cuda.stream(stream):
+            out = torch.empty((geom.rows, geom.width), dtype=torch.uint8, device=self.device)
+            check(self.lib.gol_strip_unpack(ctypes.byref(s), buf.data_ptr(), out.data_ptr(), geom.width, 1,
+                                            stream.cuda_stream), "gol_strip_unpack")
+            host = out.cpu()
+        return host
 
 
 class StripRunner:
@@ -143,10 +149,16 @@ class StripRunner:
             raise ValueError(f"temporal block k={k} is not supported for interleave {ilv}")
         self.geom = Geometry(width, height, y0, rows, 0 if single else k, width // 32, boundary,
                              wrap_rows=single and boundary == TORUS, ilv=ilv)
-        self.bufs = [self.engine.alloc(self.geom), self.engine.alloc(self.geom)]
+        self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else _NullStream()
+        # the two k-row edge bands run on their own stream: they wait only for the halo exchange, so they
+        # fill the tail of the interior launch instead of queueing behind it
+        self.edge_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else _NullStream()
+        self.bufs = [self.engine.alloc(self.geom, self.compute_stream), self.engine.alloc(self.geom, self.compute_stream)]
+        if self.device.type == "cuda":
+            for b in self.bufs:
+                b.record_stream(self.edge_stream)  # written by the edge stream too
         self.cur = 0
         self.generation = 0
-        self.compute_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else _NullStream()
         self.up = (rank - 1) % world if (boundary == TORUS or rank > 0) else None
         self.down = (rank + 1) % world if (boundary == TORUS or rank < world - 1) else None
         self.exchanger = exchanger if exchanger is not None else DistExchange(group)
@@ -184,12 +196,15 @@ class StripRunner:
             self.engine.step(self.geom, src, dst, k, 0, h, s)
         else:
             lo, hi = min(k, h), max(h - k, min(k, h))
+            e = self.edge_stream
+            _wait_stream(e, s)  # previous pass and any host-staged ghost copies are done
             self.engine.step(self.geom, src, dst, k, lo, hi, s)  # interior overlaps the exchange
-            with _stream_ctx(s):
+            with _stream_ctx(e):
                 for r in reqs:
-                    r.wait()  # compute stream waits for the received ghost rows
-            self.engine.step(self.geom, src, dst, k, 0, lo, s)
-            self.engine.step(self.geom, src, dst, k, hi, h, s)
+                    r.wait()  # the edge stream waits for the received ghost rows
+            self.engine.step(self.geom, src, dst, k, 0, lo, e)
+            self.engine.step(self.geom, src, dst, k, hi, h, e)
+            _wait_stream(s, e)  # the pass ends when both streams are done
         self.cur ^= 1
         self.generation += k
 
@@ -375,6 +390,11 @@ class _NullCtx:
 
     def __exit__(self, *a):
         return False
+
+
+def _wait_stream(waiter, other) -> None:
+    if isinstance(waiter, torch.cuda.Stream):
+        waiter.wait_stream(other)
 
 
 def _stream_ctx(s):

@@ -44,7 +44,7 @@ class OracleEngine:
     def ilv_for(self, width):
         return self.ilv
 
-    def alloc(self, geom):
+    def alloc(self, geom, stream=None):
         return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32)
 
     def step(self, geom, src, dst, k, out_begin, out_end, stream=None):

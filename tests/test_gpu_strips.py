@@ -34,8 +34,11 @@ def test_local_strips_large_match_single_board():
         b.seed_splitmix(seed)
         b.step(gens)
         want = b.hash()
+    with Board(w, h, tblock_k=8) as b:
+        want0 = b.seed_splitmix(seed).hash()
     lb = LocalBoard(w, h, 0, 8, 4)
     lb.seed_splitmix(seed)
+    assert lb.hash() == want0  # seeding
     lb.step(gens)
     assert lb.hash() == want
 
