@@ -146,9 +146,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint32_t* row, 
 
 // Rows per loop trip (even, and a multiple of 4 so register roles repeat every trip): enough loads in
 // flight for the memory-bound K = 1 pass, fewer for the deep passes whose registers hold the windows.
+#ifndef GOL_TRIP_ROWS_DEEP
+#define GOL_TRIP_ROWS_DEEP 4
+#endif
 template <int K, int M>
 struct TripRows {
-    static constexpr int value = (K == 1 && M == 1) ? 8 : 4;
+    static constexpr int value = (K == 1 && M == 1) ? 8 : (K * M >= 32 && M <= 2 ? GOL_TRIP_ROWS_DEEP : 4);
 };
 
 // One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
