@@ -227,7 +227,7 @@ def main():
             },
             "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure (rank 0 only)
             result["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -89,6 +89,7 @@ SIGNATURES = {
     "gol_default_ilv": (ctypes.c_int, [i64]),
     "gol_default_tblock": (ctypes.c_int, [ctypes.c_int]),
     "gol_supported_k": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "gol_fullrow_wg": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int]),
     "gol_last_error": (ctypes.c_char_p, []),
     "gol_version": (ctypes.c_char_p, []),
     "gol_strip_step": (ctypes.c_int, [sp, vp, vp, ctypes.c_int, i64, i64, vp]),

@@ -577,6 +577,11 @@ int gol_default_tblock(int ilv) {
 
 int gol_supported_k(int k, int ilv) { return gol::stream_supported(k, ilv) ? 1 : 0; }
 
+int gol_fullrow_wg(int64_t width, int ilv, int k) {
+    if (width < 32 || width % 32 || (ilv != 1 && ilv != 2 && ilv != 4)) return 0;
+    return gol::stream_fullrow_wg(width / 32, ilv, k);
+}
+
 int gol_stream(gol_board* b, void** stream) {
     if (!b || !stream) return fail(GOL_ERR_INVALID, "null argument");
     *stream = (void*)b->stream;
@@ -595,7 +600,7 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     a.ilv = s->ilv;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
-    if (waves) *waves = a.nstrips * a.nsegs;
+    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : 1);
     return GOL_OK;
 }
 

@@ -19,7 +19,7 @@ struct StreamArgs {
     int64_t nstrips;    // filled by plan_stream
     int64_t nsegs;      // filled by plan_stream
     int32_t ilv;        // words per interleaved block (gol_layout.h): 1, 2 or 4
-    int32_t pad_;
+    int32_t wg;         // filled by plan_stream: full-row workgroup waves (0 = wave strips)
 };
 
 // ---- gol_step.hip
@@ -27,6 +27,7 @@ bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 int64_t stream_strips(int64_t words, int ilv);
+int stream_fullrow_wg(int64_t words, int ilv, int k);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,

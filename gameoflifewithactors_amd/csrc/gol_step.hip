@@ -154,12 +154,29 @@ struct TripRows {
     static constexpr int value = (K == 1 && M == 1) ? 8 : (K * M >= 32 && M <= 2 ? GOL_TRIP_ROWS_DEEP : 4);
 };
 
+// Full-row workgroup mode (WG > 0): the WG * 64 lanes of one workgroup hold one whole board row (one block
+// each, nblocks == 64 * WG), so there are no halo lanes and no partial strips; the block-edge words cross
+// lanes AND waves through an LDS exchange buffer.  Per trip the rows are split into two halves; a half's
+// edge words for level g+1 are published (ds_write_b64), the workgroup meets at a barrier, and their
+// neighbours are read (ds_read) before the OTHER half's level-g arithmetic, which hides the LDS latency:
+// two barriers per level, every wave in lockstep over the same segment.
+// Exchange slot layout: [half][level parity][row in half][1 + lane], with zero pads at index 0 and N + 1
+// (the dead cells beyond a bounded board's left / right edge).
+template <int WG, int R>
+struct WgX {
+    static constexpr int N = 64 * WG;
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    u32x2_t (*x)[2][R / 2][N + 2];
+};
+
 // One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG = 0>
 struct StreamWave {
     static constexpr int R = TripRows<K, M>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
     using V = Vec<M>;
+    using X = WgX<(WG > 0 ? WG : 1), R>;
+    static constexpr int NL = 64 * (WG > 0 ? WG : 1);  // lanes of a full-row workgroup
 
     const uint32_t* __restrict__ src;
     uint32_t* __restrict__ dst;
@@ -175,22 +192,41 @@ struct StreamWave {
     // level state: two row slots (X, Y) of block row sums (s, c) and the raw centre block of slot Y
     uint32_t sX[K][M], cX[K][M], sY[K][M], cY[K][M], aY[K][M];
 
+    // full-row workgroup mode: exchange buffer and this lane's slot indices (own, left and right neighbour)
+    X xc;
+    int xme = 0, xleft = 0, xright = 0;
+
+    // `lane`: lane within the wave's strip (wave mode) or within the workgroup (full-row mode, sx = 0)
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
                                           int64_t sx, int64_t sy)
-        : src(s), dst(d), a(args), xl(lane) {
+        : src(s), dst(d), a(args), xl(lane & 63) {
         const int64_t nblocks = a.words / M;
-        const int64_t cb = sx * kInterior - 1 + lane;  // this lane's block column (may be off-board)
-        int64_t lc;
-        if (BOUNDED) {
-            const bool in = cb >= 0 && cb < nblocks;
-            colmask = in ? 0xffffffffu : 0u;
-            lc = in ? cb : 0;
-        } else {
+        if (WG > 0) {  // block == lane, every lane on the board and stored
             colmask = 0xffffffffu;
-            lc = floor_mod(cb, nblocks);
+            load_off = lane * 4 * M;
+            store_off = load_off;
+            xme = lane + 1;
+            if (BOUNDED) {  // beyond the row's ends: the zero pads
+                xleft = lane;
+                xright = lane + 2;
+            } else {  // torus: wrap within the row
+                xleft = lane == 0 ? NL : lane;
+                xright = lane == NL - 1 ? 1 : lane + 2;
+            }
+        } else {
+            const int64_t cb = sx * kInterior - 1 + lane;  // this lane's block column (may be off-board)
+            int64_t lc;
+            if (BOUNDED) {
+                const bool in = cb >= 0 && cb < nblocks;
+                colmask = in ? 0xffffffffu : 0u;
+                lc = in ? cb : 0;
+            } else {
+                colmask = 0xffffffffu;
+                lc = floor_mod(cb, nblocks);
+            }
+            load_off = (int)(lc * 4 * M);
+            store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
         }
-        load_off = (int)(lc * 4 * M);
-        store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
         row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
@@ -253,9 +289,75 @@ struct StreamWave {
 
     // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
+    // ---- full-row workgroup mode
+    // publish rows of half h (their block-edge words are level g's inputs), barrier, read the neighbours
+    __device__ __forceinline__ void wg_publish(const uint32_t (&v)[R][M], int g, int h, uint32_t (&L)[R],
+                                               uint32_t (&Rt)[R]) {
+#pragma unroll
+        for (int i = 0; i < R / 2; i++) {
+            const int r = h * (R / 2) + i;
+            typename X::u32x2_t e = {v[r][0], v[r][M - 1]};
+            xc.x[h][g & 1][i][xme] = e;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#pragma unroll
+        for (int i = 0; i < R / 2; i++) {
+            const int r = h * (R / 2) + i;
+            L[r] = xc.x[h][g & 1][i][xleft].y;   // left neighbour's last word
+            Rt[r] = xc.x[h][g & 1][i][xright].x;  // right neighbour's first word
+        }
+    }
+
+    // level g over the two rows of half h (the same arithmetic as the wave-mode pair below)
+    __device__ __forceinline__ void wg_half(uint32_t (&v)[R][M], int g, int h, int64_t lyt, const uint32_t (&L)[R],
+                                            const uint32_t (&Rt)[R]) {
+#pragma unroll
+        for (int r = h * (R / 2); r < (h + 1) * (R / 2); r += 2) {
+            uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
+            if (BOUNDED) {
+                const int64_t gy = a.y0 + lyt + r - g - 1;
+                m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
+                m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
+            }
+            uint32_t o0[M], o1[M];
+            level_row(v[r], L[r], Rt[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+            level_row(v[r + 1], L[r + 1], Rt[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1, o1);
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                aY[g][j] = v[r + 1][j];
+                v[r][j] = o0[j];
+                v[r + 1][j] = o1[j];
+            }
+        }
+    }
+
+    template <bool SKIP>
+    __device__ __forceinline__ void process_wg(uint32_t (&v)[R][M], int64_t t) {
+        const int64_t lyt = ly0 + t * R;
+        uint32_t L[R], Rt[R];
+        wg_publish(v, 0, 0, L, Rt);
+        wg_publish(v, 0, 1, L, Rt);
+#pragma unroll
+        for (int g = 0; g < K; g++) {
+            if (SKIP && t * R + R - 1 < 2 * g) break;  // this and every deeper level is pipeline fill
+            const bool next = g + 1 < K && !(SKIP && t * R + R - 1 < 2 * (g + 1));
+            wg_half(v, g, 0, lyt, L, Rt);
+            if (next) wg_publish(v, g + 1, 0, L, Rt);  // its reads overlap the other half's arithmetic
+            wg_half(v, g, 1, lyt, L, Rt);
+            if (next) wg_publish(v, g + 1, 1, L, Rt);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
     template <bool SKIP>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
         if (GOL_DEBUG_MODE == 2) return;
+        if constexpr (WG > 0) {
+            process_wg<SKIP>(v, t);
+            return;
+        }
         const int64_t lyt = ly0 + t * R;
 #if GOL_EARLY_XLANE
         uint32_t right[R];
@@ -350,19 +452,43 @@ struct MinWaves {
 #endif
 };
 
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
-__global__ __launch_bounds__(kWave* kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(MinWaves<K, M>::value)))
-void gol_stream_step(const uint32_t* __restrict__ src,
-                                                                          uint32_t* __restrict__ dst,
-                                                                          StreamArgs a) {
-    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS>;
+// WG = 0: wave strips (kWavesPerBlock waves per workgroup, each its own column strip and segment).
+// WG > 0: full-row workgroups of WG waves (one segment per workgroup; requires words / M == 64 * WG).
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG>
+__global__ __launch_bounds__(kWave*(WG > 0 ? WG : kWavesPerBlock))
+__attribute__((amdgpu_waves_per_eu(MinWaves<K, M>::value)))
+void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
+    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS, WG>;
     constexpr int R = W::R;
     const int lane = threadIdx.x & (kWave - 1);
-    // wave index made provably uniform so all row bookkeeping lives in SGPRs
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    if (gw >= a.nstrips * a.nsegs) return;
-    W w(src, dst, a, lane, gw % a.nstrips, gw / a.nstrips);
+    int64_t sx, sy;
+    int strip_lane;
+    if constexpr (WG > 0) {
+        if ((int64_t)blockIdx.x >= a.nsegs) return;  // uniform over the workgroup
+        sx = 0;
+        sy = blockIdx.x;
+        strip_lane = threadIdx.x;
+    } else {
+        // wave index made provably uniform so all row bookkeeping lives in SGPRs
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+        if (gw >= a.nstrips * a.nsegs) return;
+        sx = gw % a.nstrips;
+        sy = gw / a.nstrips;
+        strip_lane = lane;
+    }
+    W w(src, dst, a, strip_lane, sx, sy);
+    if constexpr (WG > 0) {
+        __shared__ typename W::X::u32x2_t xbuf[2][2][R / 2][64 * WG + 2];
+        constexpr int npad = 2 * 2 * (R / 2);
+        if ((int)threadIdx.x < 2 * npad) {  // zero pads: the dead cells beyond a bounded row's ends
+            const int q = threadIdx.x >> 1;
+            const typename W::X::u32x2_t z = {0u, 0u};
+            xbuf[q / R][(q / (R / 2)) & 1][q % (R / 2)][(threadIdx.x & 1) ? 64 * WG + 1 : 0] = z;
+        }
+        w.xc.x = xbuf;
+        __syncthreads();
+    }
 
     const int64_t ntrips = (w.nsteps + R - 1) / R;
     const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
@@ -422,6 +548,13 @@ void gol_stream_step(const uint32_t* __restrict__ src,
     X(1, 2) X(2, 2) X(4, 2) X(8, 2) X(12, 2) X(16, 2)                                                    \
     X(1, 4) X(2, 4) X(4, 4) X(6, 4) X(8, 4)
 
+// Full-row workgroup instantiations (K, M, WG): the row is exactly 64 * WG blocks of M words
+// (65536 cells for (M = 4, WG = 8) and (M = 2, WG = 16)).  WG waves must fit one CU at the kernel's
+// occupancy: 8 waves need <= 256 VGPRs (2 waves/SIMD), 16 need <= 128.  Opt-in (GOL_FULLROW=1): bit-exact,
+// but the two workgroup barriers per level cost more than the halo lanes they remove (65536^2:
+// (4, 8) 81-84k vs 89-91k GCUPS in wave strips, (2, 8) 70k vs 84-89k; profiles/r1/fullrow_sweep.log).
+#define GOL_FOR_EACH_KMW(X) X(4, 4, 8) X(8, 4, 8) X(8, 2, 16)
+
 bool stream_supported(int k, int ilv) {
 #define GOL_SUP(K_, M_) \
     if (k == K_ && ilv == M_) return true;
@@ -441,54 +574,80 @@ int stream_largest_k(int64_t n, int cap, int ilv) {
 
 // Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
 // (never wraps: rows beyond the board are masked dead).
-template <int K, int M>
+template <int K, int M, int WG>
 static const void* stream_kernel(bool bounded, bool wrap) {
-    if (bounded) return (const void*)&gol_stream_step<K, M, true, false>;
-    return wrap ? (const void*)&gol_stream_step<K, M, false, true> : (const void*)&gol_stream_step<K, M, false, false>;
+    if (bounded) return (const void*)&gol_stream_step<K, M, true, false, WG>;
+    return wrap ? (const void*)&gol_stream_step<K, M, false, true, WG>
+                : (const void*)&gol_stream_step<K, M, false, false, WG>;
 }
 
-static const void* kernel_for(int k, int ilv, bool bounded, bool wrap) {
+static const void* kernel_for(int k, int ilv, int wg, bool bounded, bool wrap) {
+    if (wg == 0) {
 #define GOL_KPTR(K_, M_) \
-    if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap);
-    GOL_FOR_EACH_KM(GOL_KPTR)
+    if (k == K_ && ilv == M_) return stream_kernel<K_, M_, 0>(bounded, wrap);
+        GOL_FOR_EACH_KM(GOL_KPTR)
 #undef GOL_KPTR
+    }
+#define GOL_KWPTR(K_, M_, W_) \
+    if (k == K_ && ilv == M_ && wg == W_) return stream_kernel<K_, M_, W_>(bounded, wrap);
+    GOL_FOR_EACH_KMW(GOL_KWPTR)
+#undef GOL_KWPTR
     return nullptr;
+}
+
+// Full-row workgroup size for a row of `words` words in layout `ilv` at depth k, or 0 (wave strips).
+// GOL_FULLROW=1 enables the mode (experimental until measured).
+int stream_fullrow_wg(int64_t words, int ilv, int k) {
+    static const bool enabled = [] {
+        const char* e = std::getenv("GOL_FULLROW");
+        return e && e[0] == '1';
+    }();
+    if (!enabled || words % ilv) return 0;
+#define GOL_FR(K_, M_, W_) \
+    if (k == K_ && ilv == M_ && words / M_ == 64 * W_) return W_;
+    GOL_FOR_EACH_KMW(GOL_FR)
+#undef GOL_FR
+    return 0;
 }
 
 int64_t stream_strips(int64_t words, int ilv) { return (words / ilv + kInterior - 1) / kInterior; }
 
-// Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.
-// Falls back to 4096 when no device answers (host-only planning, e.g. CPU tests).
-static int64_t resident_waves(int k, int ilv, bool bounded, bool wrap) {
-    static std::atomic<int64_t> cache[33][5][2][2];
-    if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return 4096;
+// Scheduling units of a stream-kernel variant the current device holds at once (occupancy x CUs):
+// waves in wave mode, workgroups in full-row mode; cached.  Falls back to 4096 waves (or 256
+// workgroups) when no device answers (host-only planning, e.g. CPU tests).
+static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
+    static std::atomic<int64_t> cache[33][5][17][2][2];
+    const int64_t fallback = wg ? 256 : 4096;
+    if (k < 0 || k > 32 || ilv < 1 || ilv > 4 || wg < 0 || wg > 16) return fallback;
     if (bounded) wrap = false;
-    int64_t v = cache[k][ilv][bounded][wrap].load(std::memory_order_relaxed);
+    int64_t v = cache[k][ilv][wg][bounded][wrap].load(std::memory_order_relaxed);
     if (v > 0) return v;
-    const void* fn = kernel_for(k, ilv, bounded, wrap);
+    const void* fn = kernel_for(k, ilv, wg, bounded, wrap);
+    const int threads = kWave * (wg ? wg : kWavesPerBlock);
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kWave * kWavesPerBlock, 0) != hipSuccess ||
-        blocks <= 0 || cus <= 0) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, 0) != hipSuccess || blocks <= 0 ||
+        cus <= 0) {
         (void)hipGetLastError();
-        return 4096;
+        return fallback;
     }
-    v = (int64_t)blocks * cus * kWavesPerBlock;
-    cache[k][ilv][bounded][wrap].store(v, std::memory_order_relaxed);
+    v = (int64_t)blocks * cus * (wg ? 1 : kWavesPerBlock);
+    cache[k][ilv][wg][bounded][wrap].store(v, std::memory_order_relaxed);
     return v;
 }
 
-// Work decomposition: nstrips column strips x nsegs row segments, one wave each.  The segment count
-// makes the grid ONE balanced round of resident waves (a partial second round would leave a tail of
-// lone waves), with segments no shorter than 2K rows (pipeline fill cost).  GOL_SEG_ROWS overrides the
-// segment length (experiments).
+// Work decomposition: nstrips column strips x nsegs row segments, one wave each (full-row mode: one
+// strip, one workgroup per segment).  The segment count makes the grid ONE balanced round of resident
+// units (a partial second round would leave a tail of lone waves), with segments no shorter than 2K
+// rows (pipeline fill cost).  GOL_SEG_ROWS overrides the segment length (experiments).
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     static const int64_t env_seg = [] {
         const char* e = std::getenv("GOL_SEG_ROWS");
         return e ? std::atoll(e) : 0LL;
     }();
-    a.nstrips = stream_strips(a.words, a.ilv);
+    a.wg = stream_fullrow_wg(a.words, a.ilv, k);
+    a.nstrips = a.wg ? 1 : stream_strips(a.words, a.ilv);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
         a.nsegs = 0;
@@ -497,7 +656,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     int64_t seg = env_seg;
     if (seg <= 0) {
-        const int64_t slots = resident_waves(k, a.ilv, bounded, wrap);
+        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap);
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
         const int64_t min_seg = 2 * k > 16 ? 2 * k : 16;
@@ -509,19 +668,26 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     a.nsegs = (rows + seg - 1) / seg;
 }
 
-template <int K, int M>
-static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
-                            hipStream_t s) {
-    const int64_t waves = a.nstrips * a.nsegs;
-    const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-    const dim3 block(kWave * kWavesPerBlock);
+template <int K, int M, int WG>
+static hipError_t launch_kmw(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
+                             hipStream_t s) {
+    unsigned blocks;
+    dim3 block;
+    if (WG > 0) {
+        blocks = (unsigned)a.nsegs;
+        block = dim3(kWave * WG);
+    } else {
+        const int64_t waves = a.nstrips * a.nsegs;
+        blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+        block = dim3(kWave * kWavesPerBlock);
+    }
     if (bounded) {
-        hipLaunchKernelGGL((gol_stream_step<K, M, true, false>), dim3(blocks), block, 0, s, src, dst, a);
+        hipLaunchKernelGGL((gol_stream_step<K, M, true, false, WG>), dim3(blocks), block, 0, s, src, dst, a);
     } else {
         if (wrap)
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, true>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, true, WG>), dim3(blocks), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, false, WG>), dim3(blocks), block, 0, s, src, dst, a);
     }
     return hipGetLastError();
 }
@@ -530,8 +696,15 @@ hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, 
                               hipStream_t s) {
     plan_stream(a, k, bounded, wrap);
     if (a.nsegs <= 0) return hipSuccess;
+    if (a.wg > 0) {
+#define GOL_LAUNCH_W(K_, M_, W_) \
+    if (k == K_ && a.ilv == M_ && a.wg == W_) return launch_kmw<K_, M_, W_>(src, dst, a, bounded, wrap, s);
+        GOL_FOR_EACH_KMW(GOL_LAUNCH_W)
+#undef GOL_LAUNCH_W
+        return hipErrorInvalidValue;
+    }
 #define GOL_LAUNCH(K_, M_) \
-    if (k == K_ && a.ilv == M_) return launch_km<K_, M_>(src, dst, a, bounded, wrap, s);
+    if (k == K_ && a.ilv == M_) return launch_kmw<K_, M_, 0>(src, dst, a, bounded, wrap, s);
     GOL_FOR_EACH_KM(GOL_LAUNCH)
 #undef GOL_LAUNCH
     return hipErrorInvalidValue;

@@ -97,6 +97,10 @@ int gol_layout(gol_board* b, int* ilv, int64_t* pitch);
 int gol_default_ilv(int64_t width);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
+/* Step-kernel decomposition the engine uses for a row of `width` cells in layout `ilv` at depth k:
+ * the number of waves in a full-row workgroup (the row's blocks spread over one workgroup, block edges
+ * exchanged through LDS), or 0 for per-wave column strips. */
+int gol_fullrow_wg(int64_t width, int ilv, int k);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller. */
 int gol_stream(gol_board* b, void** stream);
 
