@@ -34,10 +34,10 @@ VALU_PEAK_TSLOTS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 def valu_slots_per_word_gen(ilv: int) -> float:
     """Algorithmic VALU issue slots per 32-cell word per generation (gol_bitlogic.h, gol_step.hip): 9
-    full-rate v_bitop3_b32 per word, plus per block of `ilv` words 2 v_alignbit_b32 and 1 DPP move, which
-    are half-rate on gfx950 (2 slots each; profiles/r1/valu_rates_gfx950.jsonl).  The block's second
-    cross-lane move is a ds_bpermute on the LDS pipe (no VALU slot)."""
-    return 9 + 6 / ilv
+    full-rate v_bitop3_b32 per word, plus per block of `ilv` words 2 v_alignbit_b32 and 2 DPP moves (the
+    block-edge words of both neighbour lanes), which are half-rate on gfx950 (2 slots each;
+    profiles/r1/valu_rates_gfx950.jsonl)."""
+    return 9 + 8 / ilv
 
 
 def parse():

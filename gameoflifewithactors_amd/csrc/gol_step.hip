@@ -33,10 +33,12 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 
 // Cross-lane exchange of the block-edge words.  Measured on gfx950 (tools/ubench/valu_rates.hip,
 // profiles/r1/valu_rates_gfx950.jsonl): a DPP move costs a half-rate VALU issue slot; ds_bpermute_b32
-// runs on the LDS pipe (no VALU slot, longer latency).  GOL_XLANE:
-//   0 = DPP both directions, 1 = ds_bpermute both directions, 2 = left via DPP, right via ds_bpermute
+// runs on the LDS pipe (no VALU slot, but ~60+ cycles of latency that the waves end up waiting on).
+// GOL_XLANE: 0 = DPP both directions, 1 = ds_bpermute both directions, 2 = left via DPP, right via
+// ds_bpermute.  With the level-fenced schedule, 0 is fastest at every depth (profiles/r1/ab_xlane2.log:
+// +2-5 % over 2, 1 is 6-17 % slower).
 #ifndef GOL_XLANE
-#define GOL_XLANE 2
+#define GOL_XLANE 0
 #endif
 // GOL_BATCH_XLANE: issue a level's ds_bpermute exchanges for all rows of a trip before its arithmetic
 #ifndef GOL_BATCH_XLANE
