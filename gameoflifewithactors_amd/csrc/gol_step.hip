@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "gol_bitlogic.h"
+#include "gol_layout.h"
 #include "gol_internal.h"
 
 namespace gol {
@@ -56,6 +57,10 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 // levels, which inflates the live register set)
 #ifndef GOL_LEVEL_FENCE
 #define GOL_LEVEL_FENCE 0
+#endif
+// GOL_BREADTH: breadth-first levels (StreamWave::level_breadth)
+#ifndef GOL_BREADTH
+#define GOL_BREADTH 0
 #endif
 // GOL_PAIR_FENCE: a scheduling barrier after every row pair (strict row-pair order inside a level)
 #ifndef GOL_PAIR_FENCE
@@ -353,6 +358,78 @@ struct StreamWave {
         }
     }
 
+    // ---- breadth-first level (GOL_BREADTH): every row of the trip through one stage of the rule before
+    // any row enters the next -- row sums of all rows, then the four full-adder halves of every word,
+    // then the two tree LUTs, then the final LUT -- with scheduling barriers between stages, so each
+    // stage is R*M independent instruction chains (a VALU result is ~9 cycles from issue to use and only
+    // 2-3 waves share a SIMD: profiles/r1/ilp_rates_gfx950.jsonl).
+    __device__ __forceinline__ void level_breadth(uint32_t (&v)[R][M], int g, int64_t lyt) {
+        constexpr int G = GOL_BREADTH > 0 ? GOL_BREADTH : 2;  // rows per breadth-first group
+        static_assert(R % G == 0 && G % 2 == 0, "groups of an even number of rows");
+        uint32_t sN[R][M], cN[R][M], vin[R][M];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) vin[r][j] = v[r][j];
+#pragma unroll
+        for (int r0 = 0; r0 < R; r0 += G) {
+#pragma unroll
+            for (int r = r0; r < r0 + G; r++)
+                row_sum_block<M>(vin[r], xl.from_left(vin[r][M - 1]), xl.from_right(vin[r][0]), sN[r], cN[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            // window of row r: P = row r-2, C = row r-1 (slots X / Y for the trip's first two rows)
+            uint32_t A[G][M], B[G][M], Xs[G][M], Ys[G][M];
+#pragma unroll
+            for (int r = r0; r < r0 + G; r++)
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const uint32_t sP = r == 0 ? sX[g][j] : (r == 1 ? sY[g][j] : sN[r - 2][j]);
+                    const uint32_t cP = r == 0 ? cX[g][j] : (r == 1 ? cY[g][j] : cN[r - 2][j]);
+                    const uint32_t sC = r == 0 ? sY[g][j] : sN[r - 1][j];
+                    const uint32_t cC = r == 0 ? cY[g][j] : cN[r - 1][j];
+                    A[r - r0][j] = lut3<0x96>(sP, sC, sN[r][j]);
+                    B[r - r0][j] = lut3<0xE8>(sP, sC, sN[r][j]);
+                    Xs[r - r0][j] = lut3<0x96>(cP, cC, cN[r][j]);
+                    Ys[r - r0][j] = lut3<0xE8>(cP, cC, cN[r][j]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t o1[G][M], o2[G][M];
+#pragma unroll
+            for (int r = r0; r < r0 + G; r++)
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const uint32_t alive = r == 0 ? aY[g][j] : vin[r - 1][j];
+                    o1[r - r0][j] = lut3<0x27>(A[r - r0][j], Ys[r - r0][j], alive);
+                    o2[r - r0][j] = lut3<0x19>(B[r - r0][j], Xs[r - r0][j], Ys[r - r0][j]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = r0; r < r0 + G; r++) {
+                uint32_t m = 0xffffffffu;
+                if (BOUNDED) {  // cells outside the board stay dead at every generation (Script.fsx:11)
+                    const int64_t gy = a.y0 + lyt + r - g - 1;
+                    m = (gy >= 0 && gy < a.height) ? colmask : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    uint32_t o = lut3<0x24>(o1[r - r0][j], o2[r - r0][j], A[r - r0][j]);
+                    if (BOUNDED) o &= m;
+                    v[r][j] = o;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // slide the window: slots X, Y <- this trip's last two rows (R is even)
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            sX[g][j] = sN[R - 2][j];
+            cX[g][j] = cN[R - 2][j];
+            sY[g][j] = sN[R - 1][j];
+            cY[g][j] = cN[R - 1][j];
+            aY[g][j] = vin[R - 1][j];
+        }
+    }
+
     template <bool SKIP>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
         if (GOL_DEBUG_MODE == 2) return;
@@ -360,6 +437,18 @@ struct StreamWave {
             process_wg<SKIP>(v, t);
             return;
         }
+#if GOL_BREADTH
+        {
+            const int64_t lyt = ly0 + t * R;
+#pragma unroll
+            for (int g = 0; g < K; g++) {
+                if (SKIP && t * R + R - 1 < 2 * g) break;
+                level_breadth(v, g, lyt);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return;
+        }
+#endif
         const int64_t lyt = ly0 + t * R;
 #if GOL_EARLY_XLANE
         uint32_t right[R];
