@@ -600,7 +600,7 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     a.ilv = s->ilv;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
-    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : 1);
+    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : (a.split > 0 ? 2 : 1));
     return GOL_OK;
 }
 

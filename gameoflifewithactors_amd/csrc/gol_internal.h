@@ -20,6 +20,9 @@ struct StreamArgs {
     int64_t nsegs;      // filled by plan_stream
     int32_t ilv;        // words per interleaved block (gol_layout.h): 1, 2 or 4
     int32_t wg;         // filled by plan_stream: full-row workgroup waves (0 = wave strips)
+    int32_t split;      // filled by plan_stream: pair split (older wave's share of a pair segment, 1/65536;
+                        // 0 = one segment per wave)
+    int32_t pad_;
 };
 
 // ---- gol_step.hip
@@ -28,6 +31,7 @@ int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 int64_t stream_strips(int64_t words, int ilv);
 int stream_fullrow_wg(int64_t words, int ilv, int k);
+int stream_pair_split(int k, int ilv);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,

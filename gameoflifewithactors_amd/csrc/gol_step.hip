@@ -66,6 +66,19 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 #ifndef GOL_PAIR_FENCE
 #define GOL_PAIR_FENCE 0
 #endif
+// GOL_FAIR_PRIO: alternate s_setprio between the two waves of a SIMD every trip (see the trip loop)
+#ifndef GOL_FAIR_PRIO
+#define GOL_FAIR_PRIO 0
+#endif
+// GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
+// into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
+#ifndef GOL_STAMP
+#define GOL_STAMP 0
+#endif
+#if GOL_STAMP
+static constexpr int kStamps = 1 << 16;
+__device__ unsigned long long g_stamps[2][kStamps];
+#endif
 // sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
 [[maybe_unused]] static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
 // GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
@@ -203,9 +216,11 @@ struct StreamWave {
     X xc;
     int xme = 0, xleft = 0, xright = 0;
 
-    // `lane`: lane within the wave's strip (wave mode) or within the workgroup (full-row mode, sx = 0)
+    // `lane`: lane within the wave's strip (wave mode) or within the workgroup (full-row mode, sx = 0).
+    // `role`: -1 = the wave owns segment sy; 0 / 1 = the older / younger wave of a SIMD pair sharing
+    // pair-segment sy (split by a.split, see plan_stream)
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
-                                          int64_t sx, int64_t sy)
+                                          int64_t sx, int64_t sy, int role = -1)
         : src(s), dst(d), a(args), xl(lane & 63) {
         const int64_t nblocks = a.words / M;
         if (WG > 0) {  // block == lane, every lane on the board and stored
@@ -237,6 +252,15 @@ struct StreamWave {
         row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
+        if (role >= 0) {  // older wave: the first `lo` rows of the pair segment, younger: the rest
+            const int64_t len = seg_end - seg_begin;
+            int64_t lo = ((int64_t)a.split * (len + 4 * K) >> 16) - 2 * K;
+            lo = lo < 0 ? 0 : (lo > len ? len : lo);
+            if (role == 0)
+                seg_end = seg_begin + lo;
+            else
+                seg_begin = seg_begin + lo;
+        }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
         ly0 = seg_begin - K;                     // level-0 row of step 0
         load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
@@ -553,7 +577,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     constexpr int R = W::R;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t sx, sy;
-    int strip_lane;
+    int strip_lane, role = -1;
     if constexpr (WG > 0) {
         if ((int64_t)blockIdx.x >= a.nsegs) return;  // uniform over the workgroup
         sx = 0;
@@ -562,13 +586,26 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     } else {
         // wave index made provably uniform so all row bookkeeping lives in SGPRs
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-        if (gw >= a.nstrips * a.nsegs) return;
-        sx = gw % a.nstrips;
-        sy = gw / a.nstrips;
+        if (a.split > 0) {  // waves w and w + kWavesPerBlock/2 share a SIMD: one pair segment between them
+            constexpr int half = kWavesPerBlock / 2;
+            const int64_t pair = (int64_t)blockIdx.x * half + wave % half;
+            role = wave / half;
+            if (pair >= a.nstrips * a.nsegs) return;
+            sx = pair % a.nstrips;
+            sy = pair / a.nstrips;
+        } else {
+            const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+            if (gw >= a.nstrips * a.nsegs) return;
+            sx = gw % a.nstrips;
+            sy = gw / a.nstrips;
+        }
         strip_lane = lane;
     }
-    W w(src, dst, a, strip_lane, sx, sy);
+    W w(src, dst, a, strip_lane, sx, sy, role);
+#if GOL_STAMP
+    const int64_t stamp_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t stamp_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if constexpr (WG > 0) {
         __shared__ typename W::X::u32x2_t xbuf[2][2][R / 2][64 * WG + 2];
         constexpr int npad = 2 * 2 * (R / 2);
@@ -598,7 +635,34 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
 #pragma unroll
         for (int j = 0; j < M; j++) B[r][j] = 0;
     w.load(A, 0);
+#if GOL_FAIR_PRIO
+    // The two waves sharing a SIMD (waves w and w + 4 of an 8-wave workgroup) do equal work, but VALU
+    // issue favours the older one: it finishes first and leaves its partner alone on the SIMD at the
+    // single-wave issue rate -- the launch tail (tools/tail.py at 65536^2, K = 16: waves 0-3 busy 489 us,
+    // waves 4-7 747 us, 81 % utilisation).  Catch-up priority: every trip each wave publishes its trip
+    // count in LDS and takes the higher issue priority while it is behind its partner (GOL_FAIR_PRIO=1),
+    // or the two alternate by trip parity (=2, measured no better).
+    __shared__ int prio_prog[64];
+    const int prio_w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int prio_q = (prio_w >> 2) & 1;
+#endif
     auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], int64_t tt, auto skip) {
+#if GOL_FAIR_PRIO == 1
+        {
+            volatile int* pp = prio_prog;
+            if (lane == 0) pp[prio_w] = (int)tt;
+            const int partner = __builtin_amdgcn_readfirstlane(pp[prio_w ^ 4]);
+            if ((int)tt <= partner)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+#elif GOL_FAIR_PRIO == 2
+        if (((tt & 1) ^ prio_q) != 0)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+#endif
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(other, tt - 1);
         w.load(other, (tt + 1) * R);
@@ -628,6 +692,13 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     (void)first_store_trip;
 #if GOL_DEBUG_MODE == 1
     if (w.dbg_acc == 0x5EED1234u) dst[lane] = w.dbg_acc;
+#endif
+#if GOL_STAMP
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0 && stamp_id < kStamps) {
+        g_stamps[0][stamp_id] = stamp_t0;
+        g_stamps[1][stamp_id] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
 }
 
@@ -703,6 +774,26 @@ int stream_fullrow_wg(int64_t words, int ilv, int k) {
 
 int64_t stream_strips(int64_t words, int ilv) { return (words / ilv + kInterior - 1) / kInterior; }
 
+// Pair split (1/65536 units): the share of a pair segment given to the older of the two waves that
+// share a SIMD.  VALU issue favours the older wave (MI355X_MICROARCH.md "Two waves per SIMD"), so with
+// equal segments it finishes early and leaves the younger alone at the single-wave issue rate
+// (tools/tail.py: 65536^2, K = 16 -- waves 0-3 of every workgroup busy 489 us, waves 4-7 747 us).
+// GOL_SPLIT=<fraction> overrides (experiments); 0 disables.
+int stream_pair_split(int k, int ilv) {
+    static const int env = [] {
+        const char* e = std::getenv("GOL_SPLIT");
+        return e ? (int)(std::atof(e) * 65536.0) : -1;
+    }();
+    if (kWavesPerBlock % 2) return 0;
+    if (env >= 0) return env;
+    // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
+    // shallow ones (short, memory-bound trips) are left unpaired
+    if (ilv == 1 && k >= 24) return (int)(0.60 * 65536);
+    if (ilv == 2 && k >= 12) return (int)(0.72 * 65536);
+    if (ilv == 4 && k >= 8) return (int)(0.55 * 65536);
+    return 0;
+}
+
 // Scheduling units of a stream-kernel variant the current device holds at once (occupancy x CUs):
 // waves in wave mode, workgroups in full-row mode; cached.  Falls back to 4096 waves (or 256
 // workgroups) when no device answers (host-only planning, e.g. CPU tests).
@@ -738,6 +829,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         return e ? std::atoll(e) : 0LL;
     }();
     a.wg = stream_fullrow_wg(a.words, a.ilv, k);
+    a.split = a.wg ? 0 : stream_pair_split(k, a.ilv);
     a.nstrips = a.wg ? 1 : stream_strips(a.words, a.ilv);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
@@ -747,10 +839,10 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     int64_t seg = env_seg;
     if (seg <= 0) {
-        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap);
+        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap) / (a.split ? 2 : 1);
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
-        const int64_t min_seg = 2 * k > 16 ? 2 * k : 16;
+        const int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * (a.split ? 2 : 1);
         const int64_t max_segs = rows / min_seg > 0 ? rows / min_seg : 1;
         if (nsegs > max_segs) nsegs = max_segs;
         seg = (rows + nsegs - 1) / nsegs;
@@ -768,7 +860,7 @@ static hipError_t launch_kmw(const uint32_t* src, uint32_t* dst, const StreamArg
         blocks = (unsigned)a.nsegs;
         block = dim3(kWave * WG);
     } else {
-        const int64_t waves = a.nstrips * a.nsegs;
+        const int64_t waves = a.nstrips * a.nsegs * (a.split ? 2 : 1);
         blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
         block = dim3(kWave * kWavesPerBlock);
     }
@@ -802,3 +894,12 @@ hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, 
 }
 
 }  // namespace gol
+
+#if GOL_STAMP
+extern "C" int gol_debug_stamps(unsigned long long* out, long long n) {
+    if (n > 2 * gol::kStamps) n = 2 * gol::kStamps;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gol::g_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif
