@@ -123,7 +123,7 @@ bool valid_k(int k) {
 }
 
 // Interleave for a packed board of this width (gol_layout.h).  Measured on MI355X at 65536^2
-// (profiles/r1/sweep_ilv.log, ab_fence2.log): ilv 2 with K = 16 is the fastest configuration, ilv 4 needs 240 window
+// (profiles/r1/sweep_ilv.log, w12_sweep*.log): ilv 2 with K = 12 is the fastest configuration, ilv 4 needs 240 window
 // VGPRs at K = 8 (2 waves/SIMD) and wastes 1/9 of its lanes on a 65536-wide row, ilv 1 pays 4x the
 // funnel shifts.  GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
 int pick_ilv(int64_t width) {
@@ -137,7 +137,7 @@ int pick_ilv(int64_t width) {
 }
 
 // Default generations per pass for a layout (measured on MI355X, DESIGN.md "Temporal block depth").
-int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 16 : 32); }
+int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 32); }
 
 }  // namespace
 
@@ -600,7 +600,7 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     a.ilv = s->ilv;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
-    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : (a.split > 0 ? 2 : 1));
+    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : (a.split > 0 ? gol::stream_wpb(k, s->ilv) / 4 : 1));
     return GOL_OK;
 }
 

@@ -31,6 +31,24 @@ static constexpr int kInterior = kWave - 2;  // blocks stored per wave column st
 #define GOL_WAVES_PER_BLOCK 8
 #endif
 static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
+// Waves per workgroup of a wave-strip kernel: 4 x the waves each SIMD holds at the kernel's register
+// footprint, so ONE workgroup fills a CU and the waves sharing a SIMD (w, w + 4, w + 8, ...) belong to the
+// same workgroup (their age order is then known: see the group split in plan_stream).  GOL_WPB_LIST
+// entries (K, M, waves) override the default; a 12-wave workgroup also asks the compiler for 3 waves/SIMD.
+#ifndef GOL_WPB_LIST
+#define GOL_WPB_LIST(X) X(12, 2, 12)
+#endif
+template <int K, int M>
+struct Wpb {
+    static constexpr int value = [] {
+        int w = kWavesPerBlock;
+#define GOL_WPB_ENTRY(K_, M_, W_) \
+    if (K == K_ && M == M_) w = W_;
+        GOL_WPB_LIST(GOL_WPB_ENTRY)
+#undef GOL_WPB_ENTRY
+        return w;
+    }();
+};
 
 // Cross-lane exchange of the block-edge words.  Measured on gfx950 (tools/ubench/valu_rates.hip,
 // profiles/r1/valu_rates_gfx950.jsonl): a DPP move costs a half-rate VALU issue slot; ds_bpermute_b32
@@ -216,6 +234,26 @@ struct StreamWave {
     X xc;
     int xme = 0, xleft = 0, xright = 0;
 
+    // First row (relative to the group segment of `len` rows) of the i-th oldest wave's share.  Shares
+    // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
+    // of a pair), applied to each wave's streamed rows (its share plus the 2K-row pipeline fill).
+    __device__ __forceinline__ int64_t group_cut(int64_t len, int i) const {
+        constexpr int n = Wpb<K, M>::value / 4;
+        if (i <= 0) return 0;
+        if (i >= n) return len;
+        const float f = (float)a.split * (1.0f / 65536.0f);
+        const float rho = (1.0f - f) / f;
+        float pw = 1.0f, sum = 0.0f, head = 0.0f;
+        for (int j = 0; j < n; j++) {
+            if (j == i) head = sum;
+            sum += pw;
+            pw *= rho;
+        }
+        const float total = (float)(len + 2 * K * n);
+        int64_t cut = (int64_t)(total * head / sum + 0.5f) - 2 * K * i;
+        return cut < 0 ? 0 : (cut > len ? len : cut);
+    }
+
     // `lane`: lane within the wave's strip (wave mode) or within the workgroup (full-row mode, sx = 0).
     // `role`: -1 = the wave owns segment sy; 0 / 1 = the older / younger wave of a SIMD pair sharing
     // pair-segment sy (split by a.split, see plan_stream)
@@ -252,14 +290,11 @@ struct StreamWave {
         row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
-        if (role >= 0) {  // older wave: the first `lo` rows of the pair segment, younger: the rest
+        if (role >= 0) {  // group segment: wave `role` (0 = oldest) takes its share, in age order
             const int64_t len = seg_end - seg_begin;
-            int64_t lo = ((int64_t)a.split * (len + 4 * K) >> 16) - 2 * K;
-            lo = lo < 0 ? 0 : (lo > len ? len : lo);
-            if (role == 0)
-                seg_end = seg_begin + lo;
-            else
-                seg_begin = seg_begin + lo;
+            const int64_t b0 = seg_begin;
+            seg_begin = b0 + group_cut(len, role);
+            seg_end = b0 + group_cut(len, role + 1);
         }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
         ly0 = seg_begin - K;                     // level-0 row of step 0
@@ -563,14 +598,14 @@ struct MinWaves {
 #ifdef GOL_MIN_WAVES
     static constexpr int value = (5 * K * M <= 96) ? 4 : (5 * K * M <= 130 ? 3 : (5 * K * M <= 200 ? 2 : 1));
 #else
-    static constexpr int value = 1;
+    static constexpr int value = Wpb<K, M>::value > 8 ? Wpb<K, M>::value / 4 : 1;
 #endif
 };
 
 // WG = 0: wave strips (kWavesPerBlock waves per workgroup, each its own column strip and segment).
 // WG > 0: full-row workgroups of WG waves (one segment per workgroup; requires words / M == 64 * WG).
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG>
-__global__ __launch_bounds__(kWave*(WG > 0 ? WG : kWavesPerBlock))
+__global__ __launch_bounds__(kWave*(WG > 0 ? WG : Wpb<K, M>::value))
 __attribute__((amdgpu_waves_per_eu(MinWaves<K, M>::value)))
 void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
     using W = StreamWave<K, M, BOUNDED, WRAP_ROWS, WG>;
@@ -586,15 +621,15 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     } else {
         // wave index made provably uniform so all row bookkeeping lives in SGPRs
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        if (a.split > 0) {  // waves w and w + kWavesPerBlock/2 share a SIMD: one pair segment between them
-            constexpr int half = kWavesPerBlock / 2;
-            const int64_t pair = (int64_t)blockIdx.x * half + wave % half;
-            role = wave / half;
-            if (pair >= a.nstrips * a.nsegs) return;
-            sx = pair % a.nstrips;
-            sy = pair / a.nstrips;
+        constexpr int WPB = Wpb<K, M>::value;
+        if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
+            const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
+            role = wave >> 2;  // 0 = the oldest
+            if (group >= a.nstrips * a.nsegs) return;
+            sx = group % a.nstrips;
+            sy = group / a.nstrips;
         } else {
-            const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+            const int64_t gw = (int64_t)blockIdx.x * WPB + wave;
             if (gw >= a.nstrips * a.nsegs) return;
             sx = gw % a.nstrips;
             sy = gw / a.nstrips;
@@ -774,6 +809,15 @@ int stream_fullrow_wg(int64_t words, int ilv, int k) {
 
 int64_t stream_strips(int64_t words, int ilv) { return (words / ilv + kInterior - 1) / kInterior; }
 
+// Waves per workgroup of the wave-strip kernel for (k, ilv) (Wpb)
+int stream_wpb(int k, int ilv) {
+#define GOL_WPBQ(K_, M_) \
+    if (k == K_ && ilv == M_) return Wpb<K_, M_>::value;
+    GOL_FOR_EACH_KM(GOL_WPBQ)
+#undef GOL_WPBQ
+    return kWavesPerBlock;
+}
+
 // Pair split (1/65536 units): the share of a pair segment given to the older of the two waves that
 // share a SIMD.  VALU issue favours the older wave (MI355X_MICROARCH.md "Two waves per SIMD"), so with
 // equal segments it finishes early and leaves the younger alone at the single-wave issue rate
@@ -784,12 +828,14 @@ int stream_pair_split(int k, int ilv) {
         const char* e = std::getenv("GOL_SPLIT");
         return e ? (int)(std::atof(e) * 65536.0) : -1;
     }();
-    if (kWavesPerBlock % 2) return 0;
+    if (stream_wpb(k, ilv) < 8) return 0;
     if (env >= 0) return env;
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
+    // (12, 2) runs 12-wave workgroups at 3 waves/SIMD: three-way groups (profiles/r1/w12_sweep*.log)
     if (ilv == 1 && k >= 24) return (int)(0.60 * 65536);
-    if (ilv == 2 && k >= 12) return (int)(0.72 * 65536);
+    if (ilv == 2 && k == 12) return (int)(0.70 * 65536);
+    if (ilv == 2 && k >= 16) return (int)(0.72 * 65536);
     if (ilv == 4 && k >= 8) return (int)(0.55 * 65536);
     return 0;
 }
@@ -805,7 +851,8 @@ static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
     int64_t v = cache[k][ilv][wg][bounded][wrap].load(std::memory_order_relaxed);
     if (v > 0) return v;
     const void* fn = kernel_for(k, ilv, wg, bounded, wrap);
-    const int threads = kWave * (wg ? wg : kWavesPerBlock);
+    const int wpb = stream_wpb(k, ilv);
+    const int threads = kWave * (wg ? wg : wpb);
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -814,7 +861,7 @@ static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
         (void)hipGetLastError();
         return fallback;
     }
-    v = (int64_t)blocks * cus * (wg ? 1 : kWavesPerBlock);
+    v = (int64_t)blocks * cus * (wg ? 1 : wpb);
     cache[k][ilv][wg][bounded][wrap].store(v, std::memory_order_relaxed);
     return v;
 }
@@ -839,10 +886,11 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     int64_t seg = env_seg;
     if (seg <= 0) {
-        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap) / (a.split ? 2 : 1);
+        const int group = a.split ? stream_wpb(k, a.ilv) / 4 : 1;  // waves per segment
+        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap) / group;
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
-        const int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * (a.split ? 2 : 1);
+        const int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * group;
         const int64_t max_segs = rows / min_seg > 0 ? rows / min_seg : 1;
         if (nsegs > max_segs) nsegs = max_segs;
         seg = (rows + nsegs - 1) / nsegs;
@@ -860,9 +908,10 @@ static hipError_t launch_kmw(const uint32_t* src, uint32_t* dst, const StreamArg
         blocks = (unsigned)a.nsegs;
         block = dim3(kWave * WG);
     } else {
-        const int64_t waves = a.nstrips * a.nsegs * (a.split ? 2 : 1);
-        blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-        block = dim3(kWave * kWavesPerBlock);
+        constexpr int WPB = Wpb<K, M>::value;
+        const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
+        blocks = (unsigned)((waves + WPB - 1) / WPB);
+        block = dim3(kWave * WPB);
     }
     if (bounded) {
         hipLaunchKernelGGL((gol_stream_step<K, M, true, false, WG>), dim3(blocks), block, 0, s, src, dst, a);
