@@ -29,7 +29,7 @@ struct StreamArgs {
 bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
-int64_t stream_strips(int64_t words, int ilv);
+int64_t stream_strips(int64_t words, int ilv, int k);
 int stream_fullrow_wg(int64_t words, int ilv, int k);
 int stream_pair_split(int k, int ilv);
 int stream_wpb(int k, int ilv);

@@ -84,6 +84,10 @@ struct Wpb {
 #ifndef GOL_PAIR_FENCE
 #define GOL_PAIR_FENCE 0
 #endif
+// GOL_K1_NOHALO: K = 1 passes use halo-free 64-block strips (StreamWave::kNoHalo)
+#ifndef GOL_K1_NOHALO
+#define GOL_K1_NOHALO 1
+#endif
 // GOL_FAIR_PRIO: alternate s_setprio between the two waves of a SIMD every trip (see the trip loop)
 #ifndef GOL_FAIR_PRIO
 #define GOL_FAIR_PRIO 0
@@ -215,6 +219,12 @@ struct StreamWave {
     using V = Vec<M>;
     using X = WgX<(WG > 0 ? WG : 1), R>;
     static constexpr int NL = 64 * (WG > 0 ? WG : 1);  // lanes of a full-row workgroup
+    // K = 1 wave strips have no halo lanes: all 64 lanes are stored, and the two words beyond the
+    // strip's ends (left of lane 0, right of lane 63) are loaded from memory with the row (one extra
+    // dword load per row; lanes 1-62 reload their own word, an L1 hit).  Stores are then whole
+    // 64-block runs: 256 / 512 / 1024 B aligned, instead of 62-block runs at 248 B offsets.
+    static constexpr bool kNoHalo = (K == 1 && WG == 0 && GOL_K1_NOHALO);
+    static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
 
     const uint32_t* __restrict__ src;
     uint32_t* __restrict__ dst;
@@ -229,6 +239,10 @@ struct StreamWave {
 
     // level state: two row slots (X, Y) of block row sums (s, c) and the raw centre block of slot Y
     uint32_t sX[K][M], cX[K][M], sY[K][M], cY[K][M], aY[K][M];
+
+    // K = 1 halo-free strips: byte offset of this lane's neighbour word, and its bounded-board mask
+    int nb_off = 0;
+    uint32_t nbmask = 0xffffffffu;
 
     // full-row workgroup mode: exchange buffer and this lane's slot indices (own, left and right neighbour)
     X xc;
@@ -274,7 +288,8 @@ struct StreamWave {
                 xright = lane == NL - 1 ? 1 : lane + 2;
             }
         } else {
-            const int64_t cb = sx * kInterior - 1 + lane;  // this lane's block column (may be off-board)
+            // this lane's block column (may be off-board)
+            const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
             int64_t lc;
             if (BOUNDED) {
                 const bool in = cb >= 0 && cb < nblocks;
@@ -285,7 +300,24 @@ struct StreamWave {
                 lc = floor_mod(cb, nblocks);
             }
             load_off = (int)(lc * 4 * M);
-            store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
+            if (kNoHalo) {
+                store_off = cb < nblocks ? load_off : kNoStore;
+                // lane 0: last word of the block to the left; lane 63: first word of the block to the right
+                const int64_t nbc = lane == 0 ? cb - 1 : (lane == kWave - 1 ? cb + 1 : lc);
+                const int nbw = lane == 0 ? M - 1 : 0;
+                int64_t nl;
+                if (BOUNDED) {
+                    const bool in = nbc >= 0 && nbc < nblocks;
+                    nbmask = in ? 0xffffffffu : 0u;
+                    nl = in ? nbc : 0;
+                } else {
+                    nbmask = 0xffffffffu;
+                    nl = floor_mod(nbc, nblocks);
+                }
+                nb_off = (int)((nl * M + nbw) * 4);
+            } else {
+                store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
+            }
         }
         row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
@@ -307,7 +339,7 @@ struct StreamWave {
 
     // Load the next R level-0 rows.  Loads are unconditional (addresses clamped, values masked) so every
     // trip issues a fixed number of memory operations and the compiler waits for exactly the loads.
-    __device__ __forceinline__ void load(uint32_t (&buf)[R][M], int64_t first_step) {
+    __device__ __forceinline__ void load(uint32_t (&buf)[R][M], uint32_t (&nb)[R], int64_t first_step) {
         const int64_t buf_rows = a.rows + 2 * a.ghost;
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -326,12 +358,15 @@ struct StreamWave {
                 buf[r][j] = ((uint32_t)load_off * 0x9E3779B9u) ^ ((uint32_t)br * 0x85EBCA6Bu + (uint32_t)j);
 #else
             V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
+            if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
 #endif
             if (BOUNDED) {
                 const int64_t gy = a.y0 + ly0 + first_step + r;
-                const uint32_t m = (gy >= 0 && gy < a.height) ? colmask : 0u;
+                const bool row_in = gy >= 0 && gy < a.height;
+                const uint32_t m = row_in ? colmask : 0u;
 #pragma unroll
                 for (int j = 0; j < M; j++) buf[r][j] &= m;
+                if (kNoHalo) nb[r] &= row_in ? nbmask : 0u;
             }
         }
     }
@@ -490,10 +525,38 @@ struct StreamWave {
     }
 
     template <bool SKIP>
-    __device__ __forceinline__ void process(uint32_t (&v)[R][M], int64_t t) {
+    __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
         if (GOL_DEBUG_MODE == 2) return;
         if constexpr (WG > 0) {
             process_wg<SKIP>(v, t);
+            return;
+        }
+        if constexpr (kNoHalo) {  // K = 1: lanes 0 / 63 keep the loaded neighbour word (bound_ctrl off)
+            const int64_t lyt = ly0 + t * R;
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
+                if (BOUNDED) {
+                    const int64_t gy = a.y0 + lyt + r - 1;
+                    m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
+                    m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
+                }
+                const uint32_t l0 = (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r], (int)v[r][M - 1], 0x138, 0xf, 0xf, false);
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r], (int)v[r][0], 0x130, 0xf, 0xf, false);
+                const uint32_t l1 =
+                    (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r + 1], (int)v[r + 1][M - 1], 0x138, 0xf, 0xf, false);
+                const uint32_t r1 =
+                    (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r + 1], (int)v[r + 1][0], 0x130, 0xf, 0xf, false);
+                uint32_t o0[M], o1[M];
+                level_row(v[r], l0, r0, sX[0], cX[0], sY[0], cY[0], aY[0], m0, o0);
+                level_row(v[r + 1], l1, r1, sY[0], cY[0], sX[0], cX[0], v[r], m1, o1);
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    aY[0][j] = v[r + 1][j];
+                    v[r][j] = o0[j];
+                    v[r + 1][j] = o1[j];
+                }
+            }
             return;
         }
 #if GOL_BREADTH
@@ -664,12 +727,14 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     // a whole trip earlier (the wait-count pass treats pending loads and stores as completing out of
     // order: waiting for a prefetched row with a younger store in flight would drain that store too),
     // and the two row buffers alternate roles (A/B) so no register copy or early wait joins a prefetch.
-    uint32_t A[R][M], B[R][M];
+    uint32_t A[R][M], B[R][M], NA[R], NB[R];  // rows and (K = 1 halo-free) neighbour words
 #pragma unroll
-    for (int r = 0; r < R; r++)
+    for (int r = 0; r < R; r++) {
+        NA[r] = NB[r] = 0;
 #pragma unroll
         for (int j = 0; j < M; j++) B[r][j] = 0;
-    w.load(A, 0);
+    }
+    w.load(A, NA, 0);
 #if GOL_FAIR_PRIO
     // The two waves sharing a SIMD (waves w and w + 4 of an 8-wave workgroup) do equal work, but VALU
     // issue favours the older one: it finishes first and leaves its partner alone on the SIMD at the
@@ -681,7 +746,8 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     const int prio_w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int prio_q = (prio_w >> 2) & 1;
 #endif
-    auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], int64_t tt, auto skip) {
+    auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
+                    int64_t tt, auto skip) {
 #if GOL_FAIR_PRIO == 1
         {
             volatile int* pp = prio_prog;
@@ -700,24 +766,24 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
 #endif
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(other, tt - 1);
-        w.load(other, (tt + 1) * R);
+        w.load(other, nother, (tt + 1) * R);
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
-        w.template process<decltype(skip)::value>(cur, tt);
+        w.template process<decltype(skip)::value>(cur, ncur, tt);
     };
     using Skip = std::true_type;
     using NoSkip = std::false_type;
     const int64_t fill_pairs = (t_fill < ntrips ? t_fill : ntrips) / 2;
     int64_t t = 0;
     for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
-        trip(A, B, t, Skip{});
-        trip(B, A, t + 1, Skip{});
+        trip(A, B, NA, NB, t, Skip{});
+        trip(B, A, NB, NA, t + 1, Skip{});
     }
     for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
-        trip(A, B, t, NoSkip{});
-        trip(B, A, t + 1, NoSkip{});
+        trip(A, B, NA, NB, t, NoSkip{});
+        trip(B, A, NB, NA, t + 1, NoSkip{});
     }
     if (t < ntrips) {  // odd trip count: one more trip, outputs land in A
-        trip(A, B, t, NoSkip{});
+        trip(A, B, NA, NB, t, NoSkip{});
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(A, t);
     } else {
@@ -807,7 +873,10 @@ int stream_fullrow_wg(int64_t words, int ilv, int k) {
     return 0;
 }
 
-int64_t stream_strips(int64_t words, int ilv) { return (words / ilv + kInterior - 1) / kInterior; }
+int64_t stream_strips(int64_t words, int ilv, int k) {
+    const int per = (k == 1 && GOL_K1_NOHALO) ? kWave : kInterior;  // K = 1: halo-free strips
+    return (words / ilv + per - 1) / per;
+}
 
 // Waves per workgroup of the wave-strip kernel for (k, ilv) (Wpb)
 int stream_wpb(int k, int ilv) {
@@ -877,7 +946,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }();
     a.wg = stream_fullrow_wg(a.words, a.ilv, k);
     a.split = a.wg ? 0 : stream_pair_split(k, a.ilv);
-    a.nstrips = a.wg ? 1 : stream_strips(a.words, a.ilv);
+    a.nstrips = a.wg ? 1 : stream_strips(a.words, a.ilv, k);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
         a.nsegs = 0;
