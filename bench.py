@@ -166,6 +166,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kernel_s = float(t[0]), float(t[1])
 
+    # Memory-side reference point, outside the timed region: the same board streamed by K = 1 passes (the
+    # halo-free streaming kernel), HIP events on the compute stream.  Single GPU only.
+    k1 = None
+    if world == 1 and k > 1:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        runner.step_pass(1)
+        e0.record(stream)
+        for _ in range(16):
+            runner.step_pass(1)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t1 = e0.elapsed_time(e1) / 1e3 / 16
+        k1 = {"bound": "hbm", "achieved": round(2 * W * args.height / 8 / t1 / 1e9, 2), "peak": HBM_PEAK_GBS,
+              "unit": "GB/s", "kernel": f"gol_stream_step<K=1, M={ilv}> (halo-free strips)",
+              "avg_launch_us": round(t1 * 1e6, 2)}
+        k1["frac"] = round(k1["achieved"] / HBM_PEAK_GBS, 4)
+
     cells = W * H
     gens = args.steps * k
     gcups = cells * gens / dt / 1e9
@@ -226,6 +244,7 @@ def main():
                 "slots_per_word_gen": slots,
             },
             "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
+            "roofline_k1_stream": k1,
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure (rank 0 only)
             result["cpu_baseline"] = cpu_baseline(args)

@@ -1,0 +1,53 @@
+// GolNative.fs -- F# P/Invoke binding of libgol_hip.so (include/gol/gol.h), for the reference's
+// GameOfLife / GameOfLifeAkka projects (add before GameOfLifeDriver.fs in GameOfLife.fsproj:59-65).
+// Not compiled in this repository (no dotnet in the build image); the same entry points are exercised
+// through ctypes by tests/. See INTEGRATION.md.
+module GolNative
+
+open System
+open System.Runtime.InteropServices
+
+[<Literal>]
+let Lib = "gol_hip"   // libgol_hip.so (Linux) / gol_hip.dll; ships next to the executable
+
+type Boundary = Torus = 0 | Bounded = 1          // GameOfLifeDriver.fs:25 | Script.fsx:11
+type InitMode = DotNetMod2 = 0 | DotNetNext2 = 1 // GameOfLifeDriver.fs:9-11,16-19 | Script.fsx:25-27
+
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_create(int64 width, int64 height, int boundary, int numGpus, int tblockK, nativeint& board)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_destroy(nativeint board)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_set_cells(nativeint board, byte[] cells, int64 len)        // cells.[x + y*W], 0/1
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_get_cells(nativeint board, byte[] cells, int64 len)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_seed_dotnet(nativeint board, int seed, int mode)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_step(nativeint board, int64 generations)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_render_gray8(nativeint board, byte[] pixels, int64 stride, byte aliveValue)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_population(nativeint board, int64& out)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_hash(nativeint board, uint64& out)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern nativeint gol_last_error()
+
+let check (what: string) rc =
+    if rc <> 0 then
+        failwithf "%s failed (%d): %s" what rc (Marshal.PtrToStringAnsi(gol_last_error()))
+
+/// One board in HBM: replaces the W*H cell agents (GameOfLifeLogic.fs:39-71).
+type Board(width: int, height: int, boundary: Boundary) =
+    let mutable h = 0n
+    do check "gol_create" (gol_create(int64 width, int64 height, int boundary, 1, 0, &h))
+    member _.Seed(seed: int, mode: InitMode) = check "gol_seed_dotnet" (gol_seed_dotnet(h, seed, int mode))
+    member _.Step(generations: int64) = check "gol_step" (gol_step(h, generations))
+    member _.GetCells() =
+        let a = Array.zeroCreate<byte> (width * height)
+        check "gol_get_cells" (gol_get_cells(h, a, int64 a.Length)); a
+    member _.Render(pixels: byte[], alive: byte) =
+        check "gol_render_gray8" (gol_render_gray8(h, pixels, int64 width, alive))
+    interface IDisposable with
+        member _.Dispose() = if h <> 0n then (gol_destroy h |> ignore; h <- 0n)
