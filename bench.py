@@ -221,7 +221,7 @@ def main():
                 "interleave": ilv,
                 "boundary": args.boundary,
                 "seed": args.seed,
-                "parallelism": f"row strips x{world}" + (" (RCCL halo exchange)" if world > 1 else ""),
+                "parallelism": f"row strips x{world}" + ((" (RCCL halo exchange)" if args.dist_backend == "nccl" else " (gloo host-staged halo)") if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

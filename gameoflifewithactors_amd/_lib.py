@@ -49,7 +49,7 @@ class Strip(ctypes.Structure):
         ("boundary", ctypes.c_int32),
         ("wrap_rows", ctypes.c_int32),
         ("ilv", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("spare_waves", ctypes.c_int32),
     ]
 
 

@@ -632,6 +632,7 @@ int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k
     a.out_end = out_end;
     a.seg = 0;
     a.ilv = s->ilv;
+    a.spare = s->spare_waves > 0 ? s->spare_waves : 0;
     GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0,
                                     (hipStream_t)stream));
     return GOL_OK;

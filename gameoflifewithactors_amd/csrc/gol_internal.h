@@ -22,7 +22,7 @@ struct StreamArgs {
     int32_t wg;         // filled by plan_stream: full-row workgroup waves (0 = wave strips)
     int32_t split;      // filled by plan_stream: pair split (older wave's share of a pair segment, 1/65536;
                         // 0 = one segment per wave)
-    int32_t pad_;
+    int32_t spare;      // waves to leave free for concurrent launches (plan_stream)
 };
 
 // ---- gol_step.hip

@@ -953,10 +953,15 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         a.seg = 1;
         return;
     }
+    // a launch too short for one full group segment per strip (e.g. a k-row halo band) runs one wave per
+    // segment: splitting a handful of rows only multiplies the pipeline fill
+    if (a.split && rows < (int64_t)(stream_wpb(k, a.ilv) / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
     int64_t seg = env_seg;
     if (seg <= 0) {
         const int group = a.split ? stream_wpb(k, a.ilv) / 4 : 1;  // waves per segment
-        const int64_t slots = resident_units(k, a.ilv, a.wg, bounded, wrap) / group;
+        int64_t units = resident_units(k, a.ilv, a.wg, bounded, wrap);
+        if (!a.wg && a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
+        const int64_t slots = units / group;
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
         const int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * group;

@@ -55,9 +55,9 @@ class Geometry:
     wrap_rows: bool
     ilv: int = 1  # words per interleaved block (include/gol/gol.h, gol_strip.ilv)
 
-    def strip(self) -> Strip:
+    def strip(self, spare_waves: int = 0) -> Strip:
         return Strip(self.width, self.height, self.y0, self.rows, self.ghost, self.pitch, self.boundary,
-                     1 if self.wrap_rows else 0, self.ilv, 0)
+                     1 if self.wrap_rows else 0, self.ilv, spare_waves)
 
     @property
     def buffer_rows(self) -> int:
@@ -91,10 +91,17 @@ class HipEngine:
             return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32, device=self.device)
 
     def step(self, geom: Geometry, src: torch.Tensor, dst: torch.Tensor, k: int, out_begin: int, out_end: int,
-             stream: torch.cuda.Stream) -> None:
-        s = geom.strip()
+             stream: torch.cuda.Stream, spare_waves: int = 0) -> None:
+        s = geom.strip(spare_waves)
         check(self.lib.gol_strip_step(ctypes.byref(s), src.data_ptr(), dst.data_ptr(), k, out_begin, out_end,
                                       stream.cuda_stream), "gol_strip_step")
+
+    def plan_waves(self, geom: Geometry, k: int, out_begin: int, out_end: int) -> int:
+        """Waves gol_strip_step launches for these output rows (gol_strip_plan)."""
+        waves, seg = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.gol_strip_plan(ctypes.byref(geom.strip()), k, out_begin, out_end, ctypes.byref(waves),
+                                      ctypes.byref(seg)), "gol_strip_plan")
+        return int(waves.value)
 
     def seed_splitmix(self, geom: Geometry, buf: torch.Tensor, seed: int, stream) -> None:
         s = geom.strip()
@@ -198,7 +205,11 @@ class StripRunner:
             lo, hi = min(k, h), max(h - k, min(k, h))
             e = self.edge_stream
             _wait_stream(e, s)  # previous pass and any host-staged ghost copies are done
-            self.engine.step(self.geom, src, dst, k, lo, hi, s)  # interior overlaps the exchange
+            # interior overlaps the exchange; it leaves room on the device for the two edge bands, which
+            # then run alongside it as soon as the ghost rows land instead of in its tail
+            plan = getattr(self.engine, "plan_waves", None)
+            spare = plan(self.geom, k, 0, lo) + plan(self.geom, k, hi, h) if plan else 0
+            self.engine.step(self.geom, src, dst, k, lo, hi, s, spare_waves=spare)
             with _stream_ctx(e):
                 for r in reqs:
                     r.wait()  # the edge stream waits for the received ghost rows

@@ -126,7 +126,8 @@ typedef struct gol_strip {
     int32_t boundary; /* GOL_TORUS | GOL_BOUNDED */
     int32_t wrap_rows;
     int32_t ilv;      /* words per interleaved block: 1, 2 or 4 (gol_default_ilv) */
-    int32_t reserved; /* 0 */
+    int32_t spare_waves; /* waves gol_strip_step leaves free for concurrent work on other streams (e.g. the
+                            halo bands of the same pass); 0 = fill the device */
 } gol_strip;
 
 /* k generations over owned rows [out_begin, out_end) from src to dst (distinct buffers, same geometry).

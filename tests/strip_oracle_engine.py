@@ -47,7 +47,7 @@ class OracleEngine:
     def alloc(self, geom, stream=None):
         return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32)
 
-    def step(self, geom, src, dst, k, out_begin, out_end, stream=None):
+    def step(self, geom, src, dst, k, out_begin, out_end, stream=None, spare_waves=0):
         if out_begin >= out_end:
             return
         g = geom.ghost
