@@ -71,26 +71,9 @@ struct Wpb {
 #ifndef GOL_EARLY_XLANE
 #define GOL_EARLY_XLANE 2
 #endif
-// GOL_LEVEL_FENCE: a scheduling barrier between generation levels (keeps the scheduler from interleaving
-// levels, which inflates the live register set)
-#ifndef GOL_LEVEL_FENCE
-#define GOL_LEVEL_FENCE 0
-#endif
-// GOL_BREADTH: breadth-first levels (StreamWave::level_breadth)
-#ifndef GOL_BREADTH
-#define GOL_BREADTH 0
-#endif
-// GOL_PAIR_FENCE: a scheduling barrier after every row pair (strict row-pair order inside a level)
-#ifndef GOL_PAIR_FENCE
-#define GOL_PAIR_FENCE 0
-#endif
 // GOL_K1_NOHALO: K = 1 passes use halo-free 64-block strips (StreamWave::kNoHalo)
 #ifndef GOL_K1_NOHALO
 #define GOL_K1_NOHALO 1
-#endif
-// GOL_FAIR_PRIO: alternate s_setprio between the two waves of a SIMD every trip (see the trip loop)
-#ifndef GOL_FAIR_PRIO
-#define GOL_FAIR_PRIO 0
 #endif
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
 // into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
@@ -103,6 +86,8 @@ __device__ unsigned long long g_stamps[2][kStamps];
 #endif
 // sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
 [[maybe_unused]] static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
+// Measured and removed: breadth-first levels (profiles/r1/ab_breadth.log), per-row-pair
+// fences (ab_fence.log), s_setprio fairness between SIMD partners (tail_*.log), 8-row trips (ab_r8.log).
 // GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
 // outputs folded into one register), 2 = no arithmetic (the pass copies the board)
 #ifndef GOL_DEBUG_MODE
@@ -188,12 +173,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint32_t* row, 
 
 // Rows per loop trip (even, and a multiple of 4 so register roles repeat every trip): enough loads in
 // flight for the memory-bound K = 1 pass, fewer for the deep passes whose registers hold the windows.
-#ifndef GOL_TRIP_ROWS_DEEP
-#define GOL_TRIP_ROWS_DEEP 4
-#endif
 template <int K, int M>
 struct TripRows {
-    static constexpr int value = (K == 1 && M == 1) ? 8 : (K * M >= 32 && M <= 2 ? GOL_TRIP_ROWS_DEEP : 4);
+    static constexpr int value = (K == 1 && M == 1) ? 8 : 4;  // 8-row deep trips: -2.5 % (ab_r8.log)
 };
 
 // Full-row workgroup mode (WG > 0): the WG * 64 lanes of one workgroup hold one whole board row (one block
@@ -452,78 +434,6 @@ struct StreamWave {
         }
     }
 
-    // ---- breadth-first level (GOL_BREADTH): every row of the trip through one stage of the rule before
-    // any row enters the next -- row sums of all rows, then the four full-adder halves of every word,
-    // then the two tree LUTs, then the final LUT -- with scheduling barriers between stages, so each
-    // stage is R*M independent instruction chains (a VALU result is ~9 cycles from issue to use and only
-    // 2-3 waves share a SIMD: profiles/r1/ilp_rates_gfx950.jsonl).
-    __device__ __forceinline__ void level_breadth(uint32_t (&v)[R][M], int g, int64_t lyt) {
-        constexpr int G = GOL_BREADTH > 0 ? GOL_BREADTH : 2;  // rows per breadth-first group
-        static_assert(R % G == 0 && G % 2 == 0, "groups of an even number of rows");
-        uint32_t sN[R][M], cN[R][M], vin[R][M];
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int j = 0; j < M; j++) vin[r][j] = v[r][j];
-#pragma unroll
-        for (int r0 = 0; r0 < R; r0 += G) {
-#pragma unroll
-            for (int r = r0; r < r0 + G; r++)
-                row_sum_block<M>(vin[r], xl.from_left(vin[r][M - 1]), xl.from_right(vin[r][0]), sN[r], cN[r]);
-            __builtin_amdgcn_sched_barrier(0);
-            // window of row r: P = row r-2, C = row r-1 (slots X / Y for the trip's first two rows)
-            uint32_t A[G][M], B[G][M], Xs[G][M], Ys[G][M];
-#pragma unroll
-            for (int r = r0; r < r0 + G; r++)
-#pragma unroll
-                for (int j = 0; j < M; j++) {
-                    const uint32_t sP = r == 0 ? sX[g][j] : (r == 1 ? sY[g][j] : sN[r - 2][j]);
-                    const uint32_t cP = r == 0 ? cX[g][j] : (r == 1 ? cY[g][j] : cN[r - 2][j]);
-                    const uint32_t sC = r == 0 ? sY[g][j] : sN[r - 1][j];
-                    const uint32_t cC = r == 0 ? cY[g][j] : cN[r - 1][j];
-                    A[r - r0][j] = lut3<0x96>(sP, sC, sN[r][j]);
-                    B[r - r0][j] = lut3<0xE8>(sP, sC, sN[r][j]);
-                    Xs[r - r0][j] = lut3<0x96>(cP, cC, cN[r][j]);
-                    Ys[r - r0][j] = lut3<0xE8>(cP, cC, cN[r][j]);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t o1[G][M], o2[G][M];
-#pragma unroll
-            for (int r = r0; r < r0 + G; r++)
-#pragma unroll
-                for (int j = 0; j < M; j++) {
-                    const uint32_t alive = r == 0 ? aY[g][j] : vin[r - 1][j];
-                    o1[r - r0][j] = lut3<0x27>(A[r - r0][j], Ys[r - r0][j], alive);
-                    o2[r - r0][j] = lut3<0x19>(B[r - r0][j], Xs[r - r0][j], Ys[r - r0][j]);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int r = r0; r < r0 + G; r++) {
-                uint32_t m = 0xffffffffu;
-                if (BOUNDED) {  // cells outside the board stay dead at every generation (Script.fsx:11)
-                    const int64_t gy = a.y0 + lyt + r - g - 1;
-                    m = (gy >= 0 && gy < a.height) ? colmask : 0u;
-                }
-#pragma unroll
-                for (int j = 0; j < M; j++) {
-                    uint32_t o = lut3<0x24>(o1[r - r0][j], o2[r - r0][j], A[r - r0][j]);
-                    if (BOUNDED) o &= m;
-                    v[r][j] = o;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // slide the window: slots X, Y <- this trip's last two rows (R is even)
-#pragma unroll
-        for (int j = 0; j < M; j++) {
-            sX[g][j] = sN[R - 2][j];
-            cX[g][j] = cN[R - 2][j];
-            sY[g][j] = sN[R - 1][j];
-            cY[g][j] = cN[R - 1][j];
-            aY[g][j] = vin[R - 1][j];
-        }
-    }
-
     template <bool SKIP>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
         if (GOL_DEBUG_MODE == 2) return;
@@ -559,18 +469,6 @@ struct StreamWave {
             }
             return;
         }
-#if GOL_BREADTH
-        {
-            const int64_t lyt = ly0 + t * R;
-#pragma unroll
-            for (int g = 0; g < K; g++) {
-                if (SKIP && t * R + R - 1 < 2 * g) break;
-                level_breadth(v, g, lyt);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            return;
-        }
-#endif
         const int64_t lyt = ly0 + t * R;
 #if GOL_EARLY_XLANE
         uint32_t right[R];
@@ -620,11 +518,8 @@ struct StreamWave {
                     __builtin_amdgcn_sched_barrier(kAllButDs);
                 }
 #endif
-#if GOL_PAIR_FENCE
-                __builtin_amdgcn_sched_barrier(0);
-#endif
             }
-#if GOL_EARLY_XLANE == 2 || GOL_LEVEL_FENCE
+#if GOL_EARLY_XLANE == 2
             __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges
 #endif
         }
@@ -658,11 +553,7 @@ struct StreamWave {
 // Minimum waves per SIMD the register allocator must fit (0 = compiler's choice), per depth and layout.
 template <int K, int M>
 struct MinWaves {
-#ifdef GOL_MIN_WAVES
-    static constexpr int value = (5 * K * M <= 96) ? 4 : (5 * K * M <= 130 ? 3 : (5 * K * M <= 200 ? 2 : 1));
-#else
     static constexpr int value = Wpb<K, M>::value > 8 ? Wpb<K, M>::value / 4 : 1;
-#endif
 };
 
 // WG = 0: wave strips (kWavesPerBlock waves per workgroup, each its own column strip and segment).
@@ -735,35 +626,8 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         for (int j = 0; j < M; j++) B[r][j] = 0;
     }
     w.load(A, NA, 0);
-#if GOL_FAIR_PRIO
-    // The two waves sharing a SIMD (waves w and w + 4 of an 8-wave workgroup) do equal work, but VALU
-    // issue favours the older one: it finishes first and leaves its partner alone on the SIMD at the
-    // single-wave issue rate -- the launch tail (tools/tail.py at 65536^2, K = 16: waves 0-3 busy 489 us,
-    // waves 4-7 747 us, 81 % utilisation).  Catch-up priority: every trip each wave publishes its trip
-    // count in LDS and takes the higher issue priority while it is behind its partner (GOL_FAIR_PRIO=1),
-    // or the two alternate by trip parity (=2, measured no better).
-    __shared__ int prio_prog[64];
-    const int prio_w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int prio_q = (prio_w >> 2) & 1;
-#endif
     auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
                     int64_t tt, auto skip) {
-#if GOL_FAIR_PRIO == 1
-        {
-            volatile int* pp = prio_prog;
-            if (lane == 0) pp[prio_w] = (int)tt;
-            const int partner = __builtin_amdgcn_readfirstlane(pp[prio_w ^ 4]);
-            if ((int)tt <= partner)
-                __builtin_amdgcn_s_setprio(1);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
-#elif GOL_FAIR_PRIO == 2
-        if (((tt & 1) ^ prio_q) != 0)
-            __builtin_amdgcn_s_setprio(1);
-        else
-            __builtin_amdgcn_s_setprio(0);
-#endif
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(other, tt - 1);
         w.load(other, nother, (tt + 1) * R);
