@@ -26,6 +26,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# depths compared by the on-box autotune, per layout (ilv)
+AUTOTUNE = {2: [12, 16], 1: [24, 32]}
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # VALU issue peak: 256 CUs x 4 SIMDs, each retiring one full-rate wave64 instruction per 2 cycles (32
 # lane-slots per cycle) at 2.4 GHz.
@@ -135,9 +138,30 @@ def main():
         W, H = args.width, args.height * world
     lib = _lib.load()
     ilv = lib.gol_default_ilv(W)
-    k = args.tblock or lib.gol_default_tblock(ilv)
-    runner = StripRunner(W, H, boundary, k, rank=rank, world=world, device=torch.device("cuda", dev))
+    # Temporal depth: --tblock, or a short on-box autotune between the depths that are within a few percent
+    # of each other across MI355X boxes (the clock of the box decides between them).
+    cands = [args.tblock] if args.tblock else AUTOTUNE.get(ilv, [lib.gol_default_tblock(ilv)])
+    runner = StripRunner(W, H, boundary, max(cands), rank=rank, world=world, device=torch.device("cuda", dev))
     runner.seed_splitmix(args.seed)
+    k, tune = cands[0], None
+    if len(cands) > 1:
+        per_gen = []
+        for kk in cands:
+            runner.step_pass(kk)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(runner.compute_stream)
+            for _ in range(4):
+                runner.step_pass(kk)
+            e1.record(runner.compute_stream)
+            torch.cuda.synchronize()
+            per_gen.append(e0.elapsed_time(e1) / (4 * kk))
+        if world > 1:  # every rank must use the same depth (ghost rows, halo messages)
+            t = torch.tensor(per_gen, dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            per_gen = [float(x) for x in t]
+        k = cands[min(range(len(cands)), key=lambda i: per_gen[i])]
+        tune = {str(kk): round(1e3 * pg, 3) for kk, pg in zip(cands, per_gen)}  # us per generation
+    runner.k = k
 
     for _ in range(args.warmup):
         runner.step_pass()
@@ -218,6 +242,7 @@ def main():
                 "width": W,
                 "height": H,
                 "generations_per_step": k,
+                "tblock_autotune_us_per_gen": tune,
                 "interleave": ilv,
                 "boundary": args.boundary,
                 "seed": args.seed,
