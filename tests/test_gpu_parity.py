@@ -341,3 +341,40 @@ def test_fullrow_workgroup_mode_matches_oracle():
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(wg > 0 for _, _, _, wg, _ in res), res
     assert all(ok for *_, ok in res), res
+
+
+_SPLIT_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+root = os.environ["GOL_TEST_ROOT"]
+sys.path[:0] = [root, os.path.join(root, "oracle")]
+import gameoflifewithactors_amd as g
+import gol_oracle as o
+out = []
+for boundary in (0, 1):
+    for w, h, k, ilv in ((4096, 1500, 12, 2), (4096, 700, 16, 2), (2048, 900, 32, 1), (4096, 600, 8, 4)):
+        b0 = (np.random.default_rng(w + h + k + boundary).random((h, w)) < 0.4).astype(np.uint8)
+        gens = 2 * k + 5
+        with g.Board(w, h, boundary, tblock_k=k, ilv=ilv) as b:
+            b.set_cells(b0).step(gens)
+            ok = bool(np.array_equal(b.get_cells(), o.c_run(b0, gens, boundary)))
+        out.append([boundary, w, h, k, ilv, ok])
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("split", ["0.95", "0.3", "0.5"])
+def test_group_split_extremes_match_oracle(split):
+    """Segments shared by the waves of a SIMD (age-ordered shares, plan_stream / group_cut) at extreme
+    split fractions -- an empty or near-empty share for some waves -- stay bit-exact (child process so
+    GOL_SPLIT takes effect)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, GOL_SPLIT=split, GOL_TEST_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", _SPLIT_SCRIPT], capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(ok for *_, ok in res), res
