@@ -21,6 +21,19 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// Every board call runs on the board's device whatever device the calling thread has current (staging
+// buffers are allocated on the current device), and restores the caller's device afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 int fail(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
@@ -415,6 +428,7 @@ int gol_destroy(gol_board* b) {
 int gol_set_cells(gol_board* b, const uint8_t* cells, int64_t len) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (!cells || len != b->W * b->H) return fail(GOL_ERR_INVALID, "cells length must be width*height");
     return set_cells_impl(b, cells);
 }
@@ -422,6 +436,7 @@ int gol_set_cells(gol_board* b, const uint8_t* cells, int64_t len) {
 int gol_get_cells(gol_board* b, uint8_t* cells, int64_t len) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (!cells || len != b->W * b->H) return fail(GOL_ERR_INVALID, "cells length must be width*height");
     return readback_impl(b, cells, b->W, 1);
 }
@@ -429,6 +444,7 @@ int gol_get_cells(gol_board* b, uint8_t* cells, int64_t len) {
 int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (!out || x < 0 || y < 0 || w < 0 || h < 0 || x + w > b->W || y + h > b->H)
         return fail(GOL_ERR_INVALID, "region outside the board");
     if (w == 0 || h == 0) return GOL_OK;
@@ -450,6 +466,7 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
 int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t alive_value) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (!pixels || stride < b->W) return fail(GOL_ERR_INVALID, "stride must be >= width");
     return readback_impl(b, pixels, stride, alive_value);
 }
@@ -457,6 +474,7 @@ int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t aliv
 int gol_seed_dotnet(gol_board* b, int32_t seed, int mode) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (mode != GOL_INIT_DOTNET_MOD2 && mode != GOL_INIT_DOTNET_NEXT2) return fail(GOL_ERR_INVALID, "bad mode");
     try {
         std::vector<uint8_t> cells((size_t)(b->W * b->H));
@@ -475,6 +493,7 @@ int gol_seed_dotnet(gol_board* b, int32_t seed, int mode) {
 int gol_seed_splitmix(gol_board* b, uint64_t seed) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (b->packed)
         GOL_HIP(gol::launch_splitmix_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, seed, b->ilv,
                                             b->stream));
@@ -487,6 +506,7 @@ int gol_seed_splitmix(gol_board* b, uint64_t seed) {
 int gol_clear(gol_board* b) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     GOL_HIP(hipMemsetAsync(b->buf[b->cur], 0, b->bytes(), b->stream));
     b->generation = 0;
     return sync(b);
@@ -495,6 +515,7 @@ int gol_clear(gol_board* b) {
 int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     try {
         std::vector<std::pair<int64_t, int64_t>> pts;
         std::string err;
@@ -514,6 +535,7 @@ int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y) {
 int gol_step(gol_board* b, int64_t generations) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     if (generations < 0) return fail(GOL_ERR_INVALID, "negative generations");
     return step_impl(b, generations);
 }
@@ -521,6 +543,7 @@ int gol_step(gol_board* b, int64_t generations) {
 int gol_generation(gol_board* b, int64_t* out) {
     if (!b || !out) return fail(GOL_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     *out = b->generation;
     return GOL_OK;
 }
@@ -528,6 +551,7 @@ int gol_generation(gol_board* b, int64_t* out) {
 int gol_synchronize(gol_board* b) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     return sync(b);
 }
 
@@ -535,6 +559,7 @@ int gol_population(gol_board* b, int64_t* out) {
     if (int rc = check_board(b)) return rc;
     if (!out) return fail(GOL_ERR_INVALID, "null out");
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     uint64_t v = 0;
     if (int rc = reduce_impl(b, false, &v)) return rc;
     *out = (int64_t)v;
@@ -545,6 +570,7 @@ int gol_hash(gol_board* b, uint64_t* out) {
     if (int rc = check_board(b)) return rc;
     if (!out) return fail(GOL_ERR_INVALID, "null out");
     std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
     return reduce_impl(b, true, out);
 }
 

@@ -378,3 +378,32 @@ def test_group_split_extremes_match_oracle(split):
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(ok for *_, ok in res), res
+
+
+def test_concurrent_calls_on_one_handle_serialise(gol):
+    """The reference's timer may re-enter updateView (GameOfLifeDriver.fs:38-40): concurrent gol_step /
+    gol_hash calls on one handle (ctypes drops the GIL) are serialised by the handle's mutex, so the
+    result equals the same number of generations run sequentially."""
+    import threading
+
+    with gol.Board(1024, 768) as b, gol.Board(1024, 768) as ref:
+        b.seed_splitmix(3)
+        ref.seed_splitmix(3)
+        errors = []
+
+        def worker():
+            try:
+                for _ in range(10):
+                    b.step(5)
+                    b.hash()
+            except Exception as ex:  # noqa: BLE001
+                errors.append(ex)
+
+        threads = [threading.Thread(target=worker) for _ in range(4)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        assert not errors
+        ref.step(200)
+        assert b.generation == 200 and b.hash() == ref.hash()
