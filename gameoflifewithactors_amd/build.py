@@ -82,5 +82,27 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tu
     return lib
 
 
+HOST_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "test_host_driver.cpp")
+HOST_TEST_EXE = os.path.join(ROOT, "tests", "cpp", "build", "test_host_driver")
+
+
+def build_host_tests(verbose: bool = True) -> str:
+    """Compile the native host-mirror test (tests/cpp/test_host_driver.cpp: include/gol/gol_host.hpp over
+    libgol_hip.so, checked against the CPU oracle object oracle/build/gol_oracle.o -- test infrastructure)."""
+    oracle_obj = os.path.join(ROOT, "oracle", "build", "gol_oracle.o")
+    deps = [HOST_TEST_SRC, os.path.join(ROOT, "include", "gol", "gol_host.hpp"), os.path.join(ROOT, "include", "gol", "gol.h"),
+            LIB, oracle_obj]
+    if not _stale(HOST_TEST_EXE, deps):
+        return HOST_TEST_EXE
+    os.makedirs(os.path.dirname(HOST_TEST_EXE), exist_ok=True)
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-pthread", "-I", os.path.join(ROOT, "include"), HOST_TEST_SRC,
+           oracle_obj, "-L", HERE, "-lgol_hip", "-Wl,-rpath,$ORIGIN/../../../gameoflifewithactors_amd", "-o",
+           HOST_TEST_EXE]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return HOST_TEST_EXE
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)

@@ -152,3 +152,14 @@ def test_update_agent_fills_pixels_like_the_reference():
             agent.post(UpdateView.Update((x + y) % 2 == 0, Location(x, y)))
     assert len(frames) == 1
     assert frames[0].tolist() == [128, 0, 128, 0, 128, 0]  # pixels[x + y*W]
+
+
+def test_native_host_mirror_fails_loudly_without_gpu():
+    """include/gol/gol_host.hpp (the C++ mirror of the reference's F# driver interface): without a GPU,
+    creating a board throws gol::Error with GOL_ERR_NO_DEVICE -- no CPU fallback."""
+    from gameoflifewithactors_amd import build as b
+
+    exe = b.build_host_tests(verbose=False)
+    out = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert '"failures": []' in out.stdout

@@ -407,3 +407,16 @@ def test_concurrent_calls_on_one_handle_serialise(gol):
         assert not errors
         ref.step(200)
         assert b.generation == 200 and b.hash() == ref.hash()
+
+
+def test_native_host_mirror_driver():
+    """The C++ host mirror (include/gol/gol_host.hpp): run() / updateView() / the render agent on the
+    reference's 100x100 board, frames equal to the oracle's (both emit modes), the timer, the error path
+    (tests/cpp/test_host_driver.cpp, built by __graft_entry__.build())."""
+    import subprocess
+
+    exe = os.path.join(HERE, "cpp", "build", "test_host_driver")
+    assert os.path.exists(exe), "build first: python -c 'import __graft_entry__ as g; g.build()'"
+    out = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert '"failures": []' in out.stdout
