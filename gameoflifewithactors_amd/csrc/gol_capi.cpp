@@ -385,7 +385,8 @@ int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : pick_ilv(width)) : 0;
-        b->tblock = tblock_k ? tblock_k : default_tblock(b->ilv);
+        // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log)
+        b->tblock = tblock_k ? tblock_k : (boundary == GOL_BOUNDED && b->ilv == 2 ? 16 : default_tblock(b->ilv));
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = hipGetDevice(&b->device);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
@@ -626,7 +627,11 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     a.ilv = s->ilv;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
-    if (waves) *waves = a.nstrips * a.nsegs * (a.wg > 0 ? a.wg : (a.split > 0 ? gol::stream_wpb(k, s->ilv) / 4 : 1));
+    if (waves)
+        *waves = a.nstrips * a.nsegs *
+                 (a.wg > 0 ? a.wg
+                           : (a.split > 0 ? gol::stream_wpb(k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4
+                                          : 1));
     return GOL_OK;
 }
 

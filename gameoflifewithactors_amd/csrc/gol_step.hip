@@ -38,10 +38,14 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 #ifndef GOL_WPB_LIST
 #define GOL_WPB_LIST(X) X(12, 2, 12)
 #endif
-template <int K, int M>
+// The list applies to the single-board torus variant only: the bounded and ghost-row variants carry a few
+// more live registers and spill at the 3-waves/SIMD register budget (profiles/r1/strip_bounded_sweep.log:
+// bounded K = 12 41k GCUPS with 12-wave workgroups, 74k with 8).
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct Wpb {
     static constexpr int value = [] {
         int w = kWavesPerBlock;
+        if (BOUNDED || !WRAP_ROWS) return w;
 #define GOL_WPB_ENTRY(K_, M_, W_) \
     if (K == K_ && M == M_) w = W_;
         GOL_WPB_LIST(GOL_WPB_ENTRY)
@@ -234,7 +238,7 @@ struct StreamWave {
     // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
     // of a pair), applied to each wave's streamed rows (its share plus the 2K-row pipeline fill).
     __device__ __forceinline__ int64_t group_cut(int64_t len, int i) const {
-        constexpr int n = Wpb<K, M>::value / 4;
+        constexpr int n = Wpb<K, M, BOUNDED, WRAP_ROWS>::value / 4;
         if (i <= 0) return 0;
         if (i >= n) return len;
         const float f = (float)a.split * (1.0f / 65536.0f);
@@ -551,16 +555,16 @@ struct StreamWave {
 // loop.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch); trip t's outputs
 // are stored at the top of trip t+1 (below).
 // Minimum waves per SIMD the register allocator must fit (0 = compiler's choice), per depth and layout.
-template <int K, int M>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct MinWaves {
-    static constexpr int value = Wpb<K, M>::value > 8 ? Wpb<K, M>::value / 4 : 1;
+    static constexpr int value = Wpb<K, M, BOUNDED, WRAP_ROWS>::value > 8 ? Wpb<K, M, BOUNDED, WRAP_ROWS>::value / 4 : 1;
 };
 
 // WG = 0: wave strips (kWavesPerBlock waves per workgroup, each its own column strip and segment).
 // WG > 0: full-row workgroups of WG waves (one segment per workgroup; requires words / M == 64 * WG).
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG>
-__global__ __launch_bounds__(kWave*(WG > 0 ? WG : Wpb<K, M>::value))
-__attribute__((amdgpu_waves_per_eu(MinWaves<K, M>::value)))
+__global__ __launch_bounds__(kWave*(WG > 0 ? WG : Wpb<K, M, BOUNDED, WRAP_ROWS>::value))
+__attribute__((amdgpu_waves_per_eu(MinWaves<K, M, BOUNDED, WRAP_ROWS>::value)))
 void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
     using W = StreamWave<K, M, BOUNDED, WRAP_ROWS, WG>;
     constexpr int R = W::R;
@@ -575,7 +579,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     } else {
         // wave index made provably uniform so all row bookkeeping lives in SGPRs
         const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        constexpr int WPB = Wpb<K, M>::value;
+        constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS>::value;
         if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
             const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
             role = wave >> 2;  // 0 = the oldest
@@ -742,10 +746,11 @@ int64_t stream_strips(int64_t words, int ilv, int k) {
     return (words / ilv + per - 1) / per;
 }
 
-// Waves per workgroup of the wave-strip kernel for (k, ilv) (Wpb)
-int stream_wpb(int k, int ilv) {
+// Waves per workgroup of the wave-strip kernel variant (Wpb)
+int stream_wpb(int k, int ilv, bool bounded, bool wrap) {
+    if (bounded || !wrap) return kWavesPerBlock;
 #define GOL_WPBQ(K_, M_) \
-    if (k == K_ && ilv == M_) return Wpb<K_, M_>::value;
+    if (k == K_ && ilv == M_) return Wpb<K_, M_, false, true>::value;
     GOL_FOR_EACH_KM(GOL_WPBQ)
 #undef GOL_WPBQ
     return kWavesPerBlock;
@@ -761,7 +766,7 @@ int stream_pair_split(int k, int ilv) {
         const char* e = std::getenv("GOL_SPLIT");
         return e ? (int)(std::atof(e) * 65536.0) : -1;
     }();
-    if (stream_wpb(k, ilv) < 8) return 0;
+    if (kWavesPerBlock < 8) return 0;
     if (env >= 0) return env;
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
@@ -784,7 +789,7 @@ static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
     int64_t v = cache[k][ilv][wg][bounded][wrap].load(std::memory_order_relaxed);
     if (v > 0) return v;
     const void* fn = kernel_for(k, ilv, wg, bounded, wrap);
-    const int wpb = stream_wpb(k, ilv);
+    const int wpb = stream_wpb(k, ilv, bounded, wrap);
     const int threads = kWave * (wg ? wg : wpb);
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
@@ -819,10 +824,11 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     // a launch too short for one full group segment per strip (e.g. a k-row halo band) runs one wave per
     // segment: splitting a handful of rows only multiplies the pipeline fill
-    if (a.split && rows < (int64_t)(stream_wpb(k, a.ilv) / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
+    const int wpb = stream_wpb(k, a.ilv, bounded, wrap);
+    if (a.split && rows < (int64_t)(wpb / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
     int64_t seg = env_seg;
     if (seg <= 0) {
-        const int group = a.split ? stream_wpb(k, a.ilv) / 4 : 1;  // waves per segment
+        const int group = a.split ? wpb / 4 : 1;  // waves per segment
         int64_t units = resident_units(k, a.ilv, a.wg, bounded, wrap);
         if (!a.wg && a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
         const int64_t slots = units / group;
@@ -846,7 +852,7 @@ static hipError_t launch_kmw(const uint32_t* src, uint32_t* dst, const StreamArg
         blocks = (unsigned)a.nsegs;
         block = dim3(kWave * WG);
     } else {
-        constexpr int WPB = Wpb<K, M>::value;
+        const int WPB = stream_wpb(K, M, bounded, wrap);
         const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
         blocks = (unsigned)((waves + WPB - 1) / WPB);
         block = dim3(kWave * WPB);
