@@ -26,8 +26,19 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# depths compared by the on-box autotune, per layout (ilv)
+# depths compared by the opt-in on-box autotune (--autotune), per layout (ilv)
 AUTOTUNE = {2: [12, 16], 1: [24, 32]}
+
+
+def default_depth(lib, ilv: int, world: int, boundary: str) -> int:
+    """Fixed default temporal depth, so the bench line and a rocprof trace of the same command run the same
+    kernel.  Single board (rows wrap in the buffer): the engine default (K = 12 at M = 2: 104.7-110.7k vs
+    99-106k GCUPS for K = 16, profiles/r1/w12_sweep*.log, bench_session3.log).  Ghost-row strips (N > 1) and
+    bounded boards at M = 2 keep 8-wave workgroups, where K = 16 is faster (97k vs 88k; bounded 78.5k vs
+    74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
+    if ilv == 2 and (world > 1 or boundary == "bounded"):
+        return 16
+    return int(lib.gol_default_tblock(ilv))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # VALU issue peak: 256 CUs x 4 SIMDs, each retiring one full-rate wave64 instruction per 2 cycles (32
@@ -55,6 +66,8 @@ def parse():
                    "262144); overrides --width/--height")
     p.add_argument("--tblock", type=int, default=0,
                    help="generations per pass (0 = the engine's default for the board layout)")
+    p.add_argument("--autotune", action="store_true",
+                   help="time the AUTOTUNE depths on the box and keep the faster (agreed across ranks)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU actor baseline sample length")
@@ -138,9 +151,14 @@ def main():
         W, H = args.width, args.height * world
     lib = _lib.load()
     ilv = lib.gol_default_ilv(W)
-    # Temporal depth: --tblock, or a short on-box autotune between the depths that are within a few percent
-    # of each other across MI355X boxes (the clock of the box decides between them).
-    cands = [args.tblock] if args.tblock else AUTOTUNE.get(ilv, [lib.gol_default_tblock(ilv)])
+    # Temporal depth: --tblock, the fixed default, or (--autotune) a short on-box race between the depths
+    # that are within a few percent of each other across MI355X boxes.
+    if args.tblock:
+        cands = [args.tblock]
+    elif args.autotune:
+        cands = AUTOTUNE.get(ilv, [default_depth(lib, ilv, world, args.boundary)])
+    else:
+        cands = [default_depth(lib, ilv, world, args.boundary)]
     runner = StripRunner(W, H, boundary, max(cands), rank=rank, world=world, device=torch.device("cuda", dev))
     runner.seed_splitmix(args.seed)
     k, tune = cands[0], None
