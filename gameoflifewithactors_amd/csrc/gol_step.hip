@@ -38,14 +38,25 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 #ifndef GOL_WPB_LIST
 #define GOL_WPB_LIST(X) X(12, 2, 12)
 #endif
-// The list applies to the single-board torus variant only: the bounded and ghost-row variants carry a few
-// more live registers and spill at the 3-waves/SIMD register budget (profiles/r1/strip_bounded_sweep.log:
-// bounded K = 12 41k GCUPS with 12-wave workgroups, 74k with 8).
+// GOL_UNIFORM_SEG: group-segment bounds moved to SGPRs (readfirstlane): 0 = never, 1 = ghost-row variant
+// (strip K = 16 96k -> 105k GCUPS, profiles/r1/ab_uniform.log), 2 = every variant (the single board loses
+// 4-8 %: its register allocation changes)
+#ifndef GOL_UNIFORM_SEG
+#define GOL_UNIFORM_SEG 1
+#endif
+// GOL_WPB_GHOST: the list also applies to the ghost-row torus strip variant (multi-GPU ranks)
+#ifndef GOL_WPB_GHOST
+#define GOL_WPB_GHOST 1
+#endif
+// The list applies to the torus variants (single board and ghost-row strips).  The bounded variant carries
+// row/column masks and spills at the 3-waves/SIMD register budget (profiles/r1/strip_bounded_sweep.log:
+// bounded K = 12 41k GCUPS with 12-wave workgroups, 74k with 8).  The ghost-row variant fits once its
+// segment bounds live in SGPRs (GOL_UNIFORM_SEG; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k).
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct Wpb {
     static constexpr int value = [] {
         int w = kWavesPerBlock;
-        if (BOUNDED || !WRAP_ROWS) return w;
+        if (BOUNDED || (!WRAP_ROWS && !GOL_WPB_GHOST)) return w;
 #define GOL_WPB_ENTRY(K_, M_, W_) \
     if (K == K_ && M == M_) w = W_;
         GOL_WPB_LIST(GOL_WPB_ENTRY)
@@ -116,6 +127,14 @@ struct XLane {
 #endif
     }
 };
+
+// A wave-uniform 64-bit value the compiler cannot prove uniform (e.g. derived from float math), moved to SGPRs
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 __device__ __forceinline__ int64_t floor_mod(int64_t a, int64_t m) {
     int64_t r = a % m;
@@ -313,6 +332,13 @@ struct StreamWave {
             const int64_t b0 = seg_begin;
             seg_begin = b0 + group_cut(len, role);
             seg_end = b0 + group_cut(len, role + 1);
+            if (GOL_UNIFORM_SEG == 2 || (GOL_UNIFORM_SEG == 1 && !WRAP_ROWS && !BOUNDED)) {
+                // the group cut is float VALU math: without this the segment bounds live in 8 VGPRs, and
+                // the ghost-row variant spills at the 3-waves/SIMD budget (a scratch reload every loop
+                // trip).  The single-board variant keeps its measured instruction stream.
+                seg_begin = uniform64(seg_begin);
+                seg_end = uniform64(seg_end);
+            }
         }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
         ly0 = seg_begin - K;                     // level-0 row of step 0
@@ -748,9 +774,9 @@ int64_t stream_strips(int64_t words, int ilv, int k) {
 
 // Waves per workgroup of the wave-strip kernel variant (Wpb)
 int stream_wpb(int k, int ilv, bool bounded, bool wrap) {
-    if (bounded || !wrap) return kWavesPerBlock;
+    if (bounded) return kWavesPerBlock;
 #define GOL_WPBQ(K_, M_) \
-    if (k == K_ && ilv == M_) return Wpb<K_, M_, false, true>::value;
+    if (k == K_ && ilv == M_) return wrap ? Wpb<K_, M_, false, true>::value : Wpb<K_, M_, false, false>::value;
     GOL_FOR_EACH_KM(GOL_WPBQ)
 #undef GOL_WPBQ
     return kWavesPerBlock;
