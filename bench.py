@@ -33,9 +33,9 @@ AUTOTUNE = {2: [12, 16], 1: [24, 32]}
 def default_depth(lib, ilv: int, world: int, boundary: str) -> int:
     """Fixed default temporal depth, so the bench line and a rocprof trace of the same command run the same
     kernel.  Single board (rows wrap in the buffer): the engine default (K = 12 at M = 2: 104.7-110.7k vs
-    99-106k GCUPS for K = 16, profiles/r1/w12_sweep*.log, bench_session3.log).  Ghost-row strips (N > 1) and
-    bounded boards at M = 2 keep 8-wave workgroups, where K = 16 is faster (97k vs 88k; bounded 78.5k vs
-    74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
+    99-106k GCUPS for K = 16, profiles/r1/w12_sweep*.log, bench_session3.log).  Ghost-row strips (N > 1):
+    K = 16 (105.1k vs 96.8k for K = 12, profiles/r1/ghost_ab2.log).  Bounded boards at M = 2 keep 8-wave
+    workgroups, where K = 16 is faster (78.5k vs 74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
     if ilv == 2 and (world > 1 or boundary == "bounded"):
         return 16
     return int(lib.gol_default_tblock(ilv))

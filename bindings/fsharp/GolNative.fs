@@ -38,10 +38,11 @@ let check (what: string) rc =
     if rc <> 0 then
         failwithf "%s failed (%d): %s" what rc (Marshal.PtrToStringAnsi(gol_last_error()))
 
-/// One board in HBM: replaces the W*H cell agents (GameOfLifeLogic.fs:39-71).
-type Board(width: int, height: int, boundary: Boundary) =
+/// One board in HBM: replaces the W*H cell agents (GameOfLifeLogic.fs:39-71).  numGpus > 1 spreads it
+/// over GPUs 0..numGpus-1 of this process as row strips (bit-identical; width must be a multiple of 32).
+type Board(width: int, height: int, boundary: Boundary, ?numGpus: int) =
     let mutable h = 0n
-    do check "gol_create" (gol_create(int64 width, int64 height, int boundary, 1, 0, &h))
+    do check "gol_create" (gol_create(int64 width, int64 height, int boundary, defaultArg numGpus 1, 0, &h))
     member _.Seed(seed: int, mode: InitMode) = check "gol_seed_dotnet" (gol_seed_dotnet(h, seed, int mode))
     member _.Step(generations: int64) = check "gol_step" (gol_step(h, generations))
     member _.GetCells() =

@@ -69,6 +69,10 @@ SIGNATURES = {
     "gol_create": (ctypes.c_int, [i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
     "gol_create_ex": (ctypes.c_int, [i64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(vp)]),
+    "gol_create_multi": (ctypes.c_int, [i64, i64, ctypes.c_int, ip, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(vp)]),
+    "gol_num_parts": (ctypes.c_int, [vp, ip]),
+    "gol_part_info": (ctypes.c_int, [vp, ctypes.c_int, ip, i64p, i64p, i64p]),
     "gol_destroy": (ctypes.c_int, [vp]),
     "gol_set_cells": (ctypes.c_int, [vp, u8p, i64]),
     "gol_get_cells": (ctypes.c_int, [vp, u8p, i64]),

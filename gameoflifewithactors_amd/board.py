@@ -31,15 +31,23 @@ class Board:
 
     boundary: ``TORUS`` (the actors' topology, GameOfLifeDriver.fs:25) or ``BOUNDED`` (Script.fsx:11).
     tblock_k: upper bound on the generations fused per kernel pass (0 = library default).
+    num_gpus: N > 1 spreads the board over devices 0..N-1 of this process as row strips with peer-copied
+              halo rows (``gol_create``; bit-identical to one GPU).
+    devices: explicit strip placement (``gol_create_multi``), e.g. ``[0, 0, 0]`` runs three strips on one GPU.
     ilv: packed layout, words per interleaved block (0 = library default for the width; 1, 2, 4).
     """
 
     def __init__(self, width: int, height: int, boundary: int = TORUS, tblock_k: int = 0, num_gpus: int = 1,
-                 ilv: int = 0):
+                 ilv: int = 0, devices=None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
-        check(self._lib.gol_create_ex(width, height, boundary, num_gpus, tblock_k, ilv, ctypes.byref(h)),
-              "gol_create")
+        if devices is not None:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            check(self._lib.gol_create_multi(width, height, boundary, devs, len(devices), tblock_k, ilv,
+                                             ctypes.byref(h)), "gol_create_multi")
+        else:
+            check(self._lib.gol_create_ex(width, height, boundary, num_gpus, tblock_k, ilv, ctypes.byref(h)),
+                  "gol_create")
         self._h = h
         self.width, self.height, self.boundary = width, height, boundary
 
@@ -142,3 +150,15 @@ class Board:
         s = ctypes.c_void_p()
         check(self._lib.gol_stream(self._h, ctypes.byref(s)), "gol_stream")
         return s.value or 0
+
+    def parts(self) -> list:
+        """Row strips of the board: [{"device", "y0", "rows", "ghost"}] (one entry for a single board)."""
+        n = ctypes.c_int()
+        check(self._lib.gol_num_parts(self._h, ctypes.byref(n)), "gol_num_parts")
+        out = []
+        for i in range(n.value):
+            d, y0, rows, ghost = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            check(self._lib.gol_part_info(self._h, i, *(ctypes.byref(x) for x in (d, y0, rows, ghost))),
+                  "gol_part_info")
+            out.append({"device": d.value, "y0": y0.value, "rows": rows.value, "ghost": ghost.value})
+        return out

@@ -13,11 +13,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgol_hip.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gol_step.hip", "gol_formats.hip", "gol_capi.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gol_step.hip", "gol_formats.hip", "gol_capi.cpp", "gol_multi.cpp")]
 HEADERS = [
     os.path.join(CSRC, "gol_bitlogic.h"),
     os.path.join(CSRC, "gol_layout.h"),
     os.path.join(CSRC, "gol_internal.h"),
+    os.path.join(CSRC, "gol_multi.h"),
     os.path.join(ROOT, "include", "gol", "gol.h"),
 ]
 ARCH = "gfx950"

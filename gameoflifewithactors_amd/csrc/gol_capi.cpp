@@ -16,6 +16,7 @@
 
 #include "../../include/gol/gol.h"
 #include "gol_internal.h"
+#include "gol_multi.h"
 
 namespace {
 
@@ -154,6 +155,10 @@ int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 32); }
 
 }  // namespace
 
+namespace gol {
+int api_fail(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace gol
+
 struct gol_board {
     std::mutex mu;
     int device = 0;
@@ -168,6 +173,7 @@ struct gol_board {
     int cur = 0;
     unsigned long long* acc = nullptr;  // device scratch accumulator
     int64_t generation = 0;
+    gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
     size_t bytes() const { return packed ? (size_t)(pitch * H) * 4 : (size_t)(W * H); }
     uint32_t* words(int i) { return static_cast<uint32_t*>(buf[i]); }
@@ -199,11 +205,13 @@ int check_board(gol_board* b) {
 }
 
 int sync(gol_board* b) {
+    if (b->multi) return b->multi->synchronize();
     GOL_HIP(hipStreamSynchronize(b->stream));
     return GOL_OK;
 }
 
 int set_cells_impl(gol_board* b, const uint8_t* host) {
+    if (b->multi) return b->multi->set_cells(host);
     const size_t n = (size_t)(b->W * b->H);
     if (!b->packed) {
         GOL_HIP(hipMemcpyAsync(b->cells(b->cur), host, n, hipMemcpyHostToDevice, b->stream));
@@ -226,6 +234,7 @@ int set_cells_impl(gol_board* b, const uint8_t* host) {
 }
 
 int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
+    if (b->multi) return b->multi->readback(host, stride, value);
     const size_t n = (size_t)(stride * b->H);
     uint8_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, n);
@@ -252,6 +261,7 @@ int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
 }
 
 int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
+    if (b->multi) return b->multi->reduce(hash, out);
     GOL_HIP(hipMemsetAsync(b->acc, 0, sizeof(unsigned long long), b->stream));
     if (b->packed) {
         if (hash)
@@ -272,6 +282,7 @@ int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
 }
 
 int step_impl(gol_board* b, int64_t gens) {
+    if (b->multi) return b->multi->step(gens, &b->generation);
     if (!b->packed) {
         for (int64_t g = 0; g < gens; g++) {
             GOL_HIP(gol::launch_bytes_step(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H,
@@ -296,6 +307,7 @@ int step_impl(gol_board* b, int64_t gens) {
 int place_points(gol_board* b, const std::vector<int64_t>& xy) {
     const int64_t n = (int64_t)xy.size() / 2;
     if (n == 0) return GOL_OK;
+    if (b->multi) return b->multi->place_points(xy);
     int64_t* d = nullptr;
     hipError_t e = hipMalloc(&d, xy.size() * sizeof(int64_t));
     if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc points");
@@ -313,6 +325,7 @@ int place_points(gol_board* b, const std::vector<int64_t>& xy) {
 }
 
 void free_board(gol_board* b) {
+    delete b->multi;
     for (auto& p : b->buf)
         if (p) (void)hipFree(p);
     if (b->acc) (void)hipFree(b->acc);
@@ -356,12 +369,13 @@ uint64_t gol_hash_finalize(uint64_t h, int64_t width, int64_t height) {
     return fmix(h ^ fmix((uint64_t)width * 0x100000001B3ULL + (uint64_t)height));
 }
 
-int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out) {
-    return gol_create_ex(width, height, boundary, num_gpus, tblock_k, 0, out);
-}
+}  // extern "C"
 
-int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, int ilv,
-                  gol_board** out) {
+namespace {
+
+// devices == nullptr: one part on the calling thread's current device
+int create_impl(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock_k, int ilv,
+                gol_board** out) {
     try {
         if (!out) return fail(GOL_ERR_INVALID, "null out");
         *out = nullptr;
@@ -370,14 +384,19 @@ int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int
         if (width > ((int64_t)1 << 40) || height > ((int64_t)1 << 40) || width * height > ((int64_t)1 << 42))
             return fail(GOL_ERR_INVALID, "board too large");
         if (boundary != GOL_TORUS && boundary != GOL_BOUNDED) return fail(GOL_ERR_INVALID, "bad boundary");
-        if (num_gpus != 1)
-            return fail(GOL_ERR_UNSUPPORTED, "num_gpus must be 1; multi-GPU runs use one process per GPU (gol_strip_*)");
+        if (n < 1 || n > 64) return fail(GOL_ERR_INVALID, "num_gpus must be 1..64");
         if (tblock_k != 0 && !valid_k(tblock_k))
             return fail(GOL_ERR_INVALID, "tblock_k must be 0 (default) or one of 1,2,4,6,8,12,16,24,32");
         if (ilv != 0 && ((ilv != 1 && ilv != 2 && ilv != 4) || width % (32 * ilv)))
             return fail(GOL_ERR_INVALID, "ilv must be 0 (auto) or 1, 2, 4 dividing the width into 32*ilv-cell blocks");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(GOL_ERR_NO_DEVICE, "no HIP device");
+        if (devices)
+            for (int i = 0; i < n; i++)
+                if (devices[i] < 0 || devices[i] >= ndev) return fail(GOL_ERR_INVALID, "device index out of range");
+        if (n > 1 && width % 32)
+            return fail(GOL_ERR_UNSUPPORTED, "a multi-GPU board needs width % 32 == 0 (bit-packed layout)");
+        if (n > 1 && height < n) return fail(GOL_ERR_INVALID, "fewer board rows than GPUs");
         gol_board* b = new gol_board();
         b->W = width;
         b->H = height;
@@ -385,11 +404,27 @@ int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : pick_ilv(width)) : 0;
-        // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log)
-        b->tblock = tblock_k ? tblock_k : (boundary == GOL_BOUNDED && b->ilv == 2 ? 16 : default_tblock(b->ilv));
+        // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log);
+        // ghost-row strips (multi-GPU) likewise (K = 16 105k vs K = 12 97k GCUPS, profiles/r1/ghost_ab2.log)
+        b->tblock = tblock_k ? tblock_k
+                             : ((boundary == GOL_BOUNDED || n > 1) && b->ilv == 2 ? 16 : default_tblock(b->ilv));
         b->pitch = b->packed ? width / 32 : 0;
-        hipError_t e = hipGetDevice(&b->device);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+        hipError_t e = devices ? hipSetDevice(devices[0]) : hipSuccess;
+        if (e == hipSuccess) e = hipGetDevice(&b->device);
+        if (e != hipSuccess) {
+            free_board(b);
+            return fail(GOL_ERR_HIP, std::string("device: ") + hipGetErrorString(e));
+        }
+        if (n > 1) {  // row strips over several devices: the multi board owns all device memory
+            b->multi = new gol::MultiBoard();
+            if (int rc = b->multi->init(width, height, boundary, devices, n, b->tblock, b->ilv)) {
+                free_board(b);
+                return rc;
+            }
+            *out = b;
+            return GOL_OK;
+        }
+        e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
         if (e != hipSuccess) {
             free_board(b);
             return fail(GOL_ERR_HIP, std::string("stream: ") + hipGetErrorString(e));
@@ -418,10 +453,76 @@ int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int
     }
 }
 
+}  // namespace
+
+extern "C" {
+
+int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out) {
+    return gol_create_ex(width, height, boundary, num_gpus, tblock_k, 0, out);
+}
+
+int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, int ilv,
+                  gol_board** out) {
+    if (num_gpus == 1) return create_impl(width, height, boundary, nullptr, 1, tblock_k, ilv, out);
+    if (num_gpus < 1 || num_gpus > 64) {
+        if (out) *out = nullptr;
+        return fail(GOL_ERR_INVALID, "num_gpus must be 1..64");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        if (out) *out = nullptr;
+        return fail(GOL_ERR_NO_DEVICE, "no HIP device");
+    }
+    if (num_gpus > ndev) {
+        if (out) *out = nullptr;
+        return fail(GOL_ERR_INVALID, "num_gpus exceeds the visible HIP devices (gol_create_multi places strips explicitly)");
+    }
+    std::vector<int> devs((size_t)num_gpus);
+    for (int i = 0; i < num_gpus; i++) devs[(size_t)i] = i;
+    return create_impl(width, height, boundary, devs.data(), num_gpus, tblock_k, ilv, out);
+}
+
+int gol_create_multi(int64_t width, int64_t height, int boundary, const int* devices, int ndevices, int tblock_k,
+                     int ilv, gol_board** out) {
+    if (!devices || ndevices < 1) {
+        if (out) *out = nullptr;
+        return fail(GOL_ERR_INVALID, "devices must list at least one device");
+    }
+    return create_impl(width, height, boundary, devices, ndevices, tblock_k, ilv, out);
+}
+
+int gol_num_parts(gol_board* b, int* n) {
+    if (!b || !n) return fail(GOL_ERR_INVALID, "null argument");
+    *n = b->multi ? b->multi->parts() : 1;
+    return GOL_OK;
+}
+
+int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* rows, int64_t* ghost) {
+    if (!b) return fail(GOL_ERR_INVALID, "null board");
+    const int n = b->multi ? b->multi->parts() : 1;
+    if (part < 0 || part >= n) return fail(GOL_ERR_INVALID, "part index out of range");
+    if (b->multi) {
+        const auto& p = b->multi->part(part);
+        if (device) *device = p.device;
+        if (y0) *y0 = p.s.y0;
+        if (rows) *rows = p.s.rows;
+        if (ghost) *ghost = p.s.ghost;
+    } else {
+        if (device) *device = b->device;
+        if (y0) *y0 = 0;
+        if (rows) *rows = b->H;
+        if (ghost) *ghost = 0;
+    }
+    return GOL_OK;
+}
+
 int gol_destroy(gol_board* b) {
     if (!b) return fail(GOL_ERR_INVALID, "null board");
     (void)hipSetDevice(b->device);
-    (void)hipStreamSynchronize(b->stream);
+    if (b->multi)
+        (void)b->multi->synchronize();
+    else
+        (void)hipStreamSynchronize(b->stream);
     free_board(b);
     return GOL_OK;
 }
@@ -449,6 +550,7 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
     if (!out || x < 0 || y < 0 || w < 0 || h < 0 || x + w > b->W || y + h > b->H)
         return fail(GOL_ERR_INVALID, "region outside the board");
     if (w == 0 || h == 0) return GOL_OK;
+    if (b->multi) return b->multi->region(x, y, w, h, out);
     uint8_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, (size_t)(w * h));
     if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc region");
@@ -495,6 +597,10 @@ int gol_seed_splitmix(gol_board* b, uint64_t seed) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
     DeviceGuard dg(b->device);
+    if (b->multi) {
+        b->generation = 0;
+        return b->multi->seed_splitmix(seed);
+    }
     if (b->packed)
         GOL_HIP(gol::launch_splitmix_packed(b->words(b->cur), b->W / 32, b->H, b->pitch, 0, 0, seed, b->ilv,
                                             b->stream));
@@ -508,6 +614,10 @@ int gol_clear(gol_board* b) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);
     DeviceGuard dg(b->device);
+    if (b->multi) {
+        b->generation = 0;
+        return b->multi->clear();
+    }
     GOL_HIP(hipMemsetAsync(b->buf[b->cur], 0, b->bytes(), b->stream));
     b->generation = 0;
     return sync(b);
@@ -611,7 +721,7 @@ int gol_fullrow_wg(int64_t width, int ilv, int k) {
 
 int gol_stream(gol_board* b, void** stream) {
     if (!b || !stream) return fail(GOL_ERR_INVALID, "null argument");
-    *stream = (void*)b->stream;
+    *stream = (void*)(b->multi ? b->multi->stream0() : b->stream);
     return GOL_OK;
 }
 

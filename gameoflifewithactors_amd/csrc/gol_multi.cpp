@@ -1,0 +1,302 @@
+// gol_multi.cpp -- a board handle spread over several GPUs of one process (see gol_multi.h).
+//
+// Replaces, for a board too large or too slow for one GPU, the same reference seam as the single board:
+// the dictionary of cell actors built by GameOfLifeDriver.fs:16-30 and ticked by updateView (L32-34).
+// The per-pass protocol (ghost rows of depth k, interior || exchange, then the edge bands) is the one the
+// one-process-per-GPU path runs over RCCL (strips.py); here the exchange is a peer copy between devices
+// of the same process, ordered by HIP events instead of a communicator.
+#include "gol_multi.h"
+
+#include <algorithm>
+
+#include "gol_internal.h"
+
+namespace gol {
+
+#define GOL_MHIP(expr)                                                                                    \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess) return api_fail(GOL_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+#define GOL_MRC(expr)              \
+    do {                           \
+        int rc_ = (expr);          \
+        if (rc_ != GOL_OK) return rc_; \
+    } while (0)
+
+namespace {
+
+// device staging buffer freed on every exit path
+struct Staging {
+    void* p = nullptr;
+    ~Staging() {
+        if (p) (void)hipFree(p);
+    }
+    int alloc(size_t n) {
+        hipError_t e = hipMalloc(&p, n ? n : 1);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return api_fail(GOL_ERR_OOM, std::string("hipMalloc staging: ") + hipGetErrorString(e));
+        }
+        return GOL_OK;
+    }
+};
+
+}  // namespace
+
+int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock, int ilv) {
+    W_ = width;
+    H_ = height;
+    boundary_ = boundary;
+    ilv_ = ilv;
+    tblock_ = tblock;
+    if (n < 2 || !devices) return api_fail(GOL_ERR_INVALID, "a multi-GPU board needs at least 2 parts");
+    if (height < n) return api_fail(GOL_ERR_INVALID, "fewer board rows than GPUs");
+    // balanced row partition: part r owns [H*r/n, H*(r+1)/n)
+    int64_t min_rows = height;
+    for (int r = 0; r < n; r++) min_rows = std::min(min_rows, height * (r + 1) / n - height * r / n);
+    // a pass of k generations reads k ghost rows on each side, which come from ONE neighbour strip
+    max_k_ = stream_largest_k(std::min<int64_t>(tblock, min_rows), tblock, ilv);
+    parts_.resize((size_t)n);
+    for (int r = 0; r < n; r++) {
+        Part& p = parts_[(size_t)r];
+        p.device = devices[r];
+        p.s.width = width;
+        p.s.height = height;
+        p.s.y0 = height * r / n;
+        p.s.rows = height * (r + 1) / n - p.s.y0;
+        p.s.ghost = max_k_;
+        p.s.pitch = width / 32;
+        p.s.boundary = boundary;
+        p.s.wrap_rows = 0;
+        p.s.ilv = ilv;
+        p.s.spare_waves = 0;
+        const bool torus = boundary == GOL_TORUS;
+        p.up = r > 0 ? r - 1 : (torus ? n - 1 : -1);
+        p.down = r < n - 1 ? r + 1 : (torus ? 0 : -1);
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipStreamCreateWithFlags(&p.compute, hipStreamNonBlocking));
+        GOL_MHIP(hipStreamCreateWithFlags(&p.edge, hipStreamNonBlocking));
+        GOL_MHIP(hipStreamCreateWithFlags(&p.copy, hipStreamNonBlocking));
+        GOL_MHIP(hipEventCreateWithFlags(&p.ev_start, hipEventDisableTiming));
+        GOL_MHIP(hipEventCreateWithFlags(&p.ev_copied, hipEventDisableTiming));
+        GOL_MHIP(hipEventCreateWithFlags(&p.ev_edge, hipEventDisableTiming));
+        const size_t bytes = (size_t)((p.s.rows + 2 * p.s.ghost) * p.s.pitch) * 4;
+        for (auto& b : p.buf) {
+            hipError_t e = hipMalloc(&b, bytes);
+            if (e != hipSuccess) {
+                b = nullptr;
+                return api_fail(GOL_ERR_OOM, std::string("hipMalloc strip: ") + hipGetErrorString(e));
+            }
+            GOL_MHIP(hipMemsetAsync(b, 0, bytes, p.compute));
+        }
+        GOL_MHIP(hipMalloc(&p.acc, 64));
+    }
+    // peer access between neighbouring parts on distinct devices (xGMI); without it the copies are staged
+    for (const Part& p : parts_)
+        for (int q : {p.up, p.down}) {
+            if (q < 0 || parts_[(size_t)q].device == p.device) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, p.device, parts_[(size_t)q].device) == hipSuccess && can) {
+                GOL_MHIP(hipSetDevice(p.device));
+                hipError_t e = hipDeviceEnablePeerAccess(parts_[(size_t)q].device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return api_fail(GOL_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+                (void)hipGetLastError();
+            }
+        }
+    return synchronize();
+}
+
+MultiBoard::~MultiBoard() {
+    for (Part& p : parts_) {
+        if (hipSetDevice(p.device) != hipSuccess) continue;
+        for (hipStream_t s : {p.compute, p.edge, p.copy})
+            if (s) (void)hipStreamSynchronize(s);
+        for (auto b : p.buf)
+            if (b) (void)hipFree(b);
+        if (p.acc) (void)hipFree(p.acc);
+        for (hipEvent_t e : {p.ev_start, p.ev_copied, p.ev_edge})
+            if (e) (void)hipEventDestroy(e);
+        for (hipStream_t s : {p.compute, p.edge, p.copy})
+            if (s) (void)hipStreamDestroy(s);
+    }
+}
+
+int MultiBoard::synchronize() {
+    for (const Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipStreamSynchronize(p.copy));
+        GOL_MHIP(hipStreamSynchronize(p.edge));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::set_cells(const uint8_t* host) {
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t n = (size_t)(p.s.rows * W_);
+        Staging st;
+        GOL_MRC(st.alloc(n));
+        GOL_MHIP(hipMemcpyAsync(st.p, host + p.s.y0 * W_, n, hipMemcpyHostToDevice, p.compute));
+        GOL_MRC(gol_strip_pack(&p.s, static_cast<const uint8_t*>(st.p), p.buf[cur_], p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::readback(uint8_t* host, int64_t stride, uint8_t value) {
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t n = (size_t)(p.s.rows * stride);
+        Staging st;
+        GOL_MRC(st.alloc(n));
+        if (stride != W_) GOL_MHIP(hipMemsetAsync(st.p, 0, n, p.compute));
+        GOL_MRC(gol_strip_unpack(&p.s, p.buf[cur_], static_cast<uint8_t*>(st.p), stride, value, p.compute));
+        GOL_MHIP(hipMemcpyAsync(host + p.s.y0 * stride, st.p, n, hipMemcpyDeviceToHost, p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::region(int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out) {
+    for (Part& p : parts_) {
+        const int64_t r0 = std::max(y, p.s.y0), r1 = std::min(y + h, p.s.y0 + p.s.rows);
+        if (r0 >= r1) continue;
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t n = (size_t)((r1 - r0) * w);
+        Staging st;
+        GOL_MRC(st.alloc(n));
+        GOL_MHIP(launch_region(p.buf[cur_] + p.s.ghost * p.s.pitch, ilv_, W_, p.s.pitch, x, r0 - p.s.y0, w, r1 - r0,
+                               static_cast<uint8_t*>(st.p), p.compute));
+        GOL_MHIP(hipMemcpyAsync(out + (r0 - y) * w, st.p, n, hipMemcpyDeviceToHost, p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::seed_splitmix(uint64_t seed) {
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MRC(gol_strip_seed_splitmix(&p.s, p.buf[cur_], seed, p.compute));
+    }
+    return synchronize();
+}
+
+int MultiBoard::clear() {
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t bytes = (size_t)((p.s.rows + 2 * p.s.ghost) * p.s.pitch) * 4;
+        GOL_MHIP(hipMemsetAsync(p.buf[cur_], 0, bytes, p.compute));
+    }
+    return synchronize();
+}
+
+int MultiBoard::place_points(const std::vector<int64_t>& xy) {
+    for (Part& p : parts_) {
+        std::vector<int64_t> mine;
+        for (size_t i = 0; i + 1 < xy.size(); i += 2)
+            if (xy[i + 1] >= p.s.y0 && xy[i + 1] < p.s.y0 + p.s.rows) {
+                mine.push_back(xy[i]);
+                mine.push_back(xy[i + 1] - p.s.y0);  // owned row
+            }
+        if (mine.empty()) continue;
+        GOL_MHIP(hipSetDevice(p.device));
+        Staging st;
+        GOL_MRC(st.alloc(mine.size() * sizeof(int64_t)));
+        GOL_MHIP(hipMemcpyAsync(st.p, mine.data(), mine.size() * sizeof(int64_t), hipMemcpyHostToDevice, p.compute));
+        GOL_MHIP(launch_set_points(p.buf[cur_] + p.s.ghost * p.s.pitch, ilv_, W_, p.s.pitch,
+                                   static_cast<const int64_t*>(st.p), (int64_t)mine.size() / 2, p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::reduce(bool hash, uint64_t* out) {
+    uint64_t sum = 0;
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipMemsetAsync(p.acc, 0, sizeof(unsigned long long), p.compute));
+        uint64_t* acc = reinterpret_cast<uint64_t*>(p.acc);
+        GOL_MRC(hash ? gol_strip_hash_partial(&p.s, p.buf[cur_], acc, p.compute)
+                     : gol_strip_population(&p.s, p.buf[cur_], acc, p.compute));
+        unsigned long long v = 0;
+        GOL_MHIP(hipMemcpyAsync(&v, p.acc, sizeof(v), hipMemcpyDeviceToHost, p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+        sum += (uint64_t)v;  // hash partials add with wrap-around
+    }
+    *out = hash ? gol_hash_finalize(sum, W_, H_) : sum;
+    return GOL_OK;
+}
+
+// One pass of k generations over every part (the ordering argument is in DESIGN.md 5):
+//   compute[i]: record ev_start (previous pass of part i complete: compute joined edge at its end)
+//   copy[i]:    wait ev_start[i]; top k owned rows -> up's bottom ghost, bottom k -> down's top ghost;
+//               record ev_copied[i]
+//   compute[i]: interior rows [k, rows-k) (needs no ghost rows, overlaps the copies)
+//   edge[i]:    wait ev_start[i], ev_copied[up], ev_copied[down]; rows [0, k) and [rows-k, rows)
+//   compute[i]: wait ev_edge[i]
+// A copy into part j's ghost rows is ordered after j's previous pass has read them: the copying part's
+// previous pass waited for j's copies, which waited for j's pass before that.
+int MultiBoard::pass(int k) {
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipEventRecord(p.ev_start, p.compute));
+    }
+    const size_t row_bytes = (size_t)W_ / 8;  // pitch == width / 32 words
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipStreamWaitEvent(p.copy, p.ev_start, 0));
+        const uint32_t* src = p.buf[cur_];
+        if (p.up >= 0) {
+            Part& u = parts_[(size_t)p.up];
+            GOL_MHIP(hipMemcpyPeerAsync(u.buf[cur_] + (u.s.ghost + u.s.rows) * u.s.pitch, u.device,
+                                        src + p.s.ghost * p.s.pitch, p.device, k * row_bytes, p.copy));
+        }
+        if (p.down >= 0) {
+            Part& d = parts_[(size_t)p.down];
+            GOL_MHIP(hipMemcpyPeerAsync(d.buf[cur_] + (d.s.ghost - k) * d.s.pitch, d.device,
+                                        src + (p.s.ghost + p.s.rows - k) * p.s.pitch, p.device, k * row_bytes,
+                                        p.copy));
+        }
+        GOL_MHIP(hipEventRecord(p.ev_copied, p.copy));
+    }
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const uint32_t* src = p.buf[cur_];
+        uint32_t* dst = p.buf[cur_ ^ 1];
+        const int64_t rows = p.s.rows;
+        const int64_t lo = std::min<int64_t>(k, rows), hi = std::max<int64_t>(rows - k, lo);
+        if (lo < hi) {
+            // leave room on the device for the two edge bands, which start as soon as the ghost rows land
+            int64_t w0 = 0, w1 = 0;
+            GOL_MRC(gol_strip_plan(&p.s, k, 0, lo, &w0, nullptr));
+            GOL_MRC(gol_strip_plan(&p.s, k, hi, rows, &w1, nullptr));
+            gol_strip s = p.s;
+            s.spare_waves = (int32_t)std::min<int64_t>(w0 + w1, 1 << 20);
+            GOL_MRC(gol_strip_step(&s, src, dst, k, lo, hi, p.compute));
+        }
+        GOL_MHIP(hipStreamWaitEvent(p.edge, p.ev_start, 0));
+        for (int q : {p.up, p.down})
+            if (q >= 0) GOL_MHIP(hipStreamWaitEvent(p.edge, parts_[(size_t)q].ev_copied, 0));
+        GOL_MRC(gol_strip_step(&p.s, src, dst, k, 0, lo, p.edge));
+        GOL_MRC(gol_strip_step(&p.s, src, dst, k, hi, rows, p.edge));
+        GOL_MHIP(hipEventRecord(p.ev_edge, p.edge));
+        GOL_MHIP(hipStreamWaitEvent(p.compute, p.ev_edge, 0));
+    }
+    cur_ ^= 1;
+    return GOL_OK;
+}
+
+int MultiBoard::step(int64_t generations, int64_t* done) {
+    while (generations > 0) {
+        const int k = stream_largest_k(generations, max_k_, ilv_);
+        GOL_MRC(pass(k));
+        generations -= k;
+        *done += k;
+    }
+    return GOL_OK;
+}
+
+}  // namespace gol

@@ -1,0 +1,64 @@
+// gol_multi.h -- one board handle over several GPUs of one process (gol_create with num_gpus > 1,
+// gol_create_multi).  Not installed; gol_capi.cpp dispatches the public entry points here.
+//
+// The reference's host is ONE process (the F# driver, GameOfLifeDriver.fs:13-41), so a drop-in that
+// spreads the board over the GPUs of a node must do it behind one handle.  Layout: row strips, part r
+// owning global rows [y0_r, y0_r + rows_r) on devices[r], in the gol_strip geometry of include/gol/gol.h
+// (ghost = tblock halo rows above and below).  Per pass of k generations each part copies its top and
+// bottom k owned rows into its neighbours' ghost rows (hipMemcpyPeerAsync: xGMI between MI355X GPUs) on a
+// copy stream, while its interior rows [k, rows-k) run on the compute stream; the two k-row edge bands run
+// on an edge stream once the ghost rows have landed.  The result is bit-identical to the single board.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gol/gol.h"
+
+namespace gol {
+
+int api_fail(int code, const std::string& msg);  // sets gol_last_error (gol_capi.cpp)
+
+class MultiBoard {
+   public:
+    struct Part {
+        int device = 0;
+        gol_strip s{};
+        uint32_t* buf[2] = {nullptr, nullptr};
+        unsigned long long* acc = nullptr;
+        hipStream_t compute = nullptr, edge = nullptr, copy = nullptr;
+        hipEvent_t ev_start = nullptr, ev_copied = nullptr, ev_edge = nullptr;
+        int up = -1, down = -1;  // neighbour parts (-1: bounded board edge)
+    };
+
+    // creates the parts; returns GOL_OK or a GOL_ERR_* code (the object is then unusable)
+    int init(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock, int ilv);
+    ~MultiBoard();
+
+    int set_cells(const uint8_t* host);
+    int readback(uint8_t* host, int64_t stride, uint8_t value);
+    int region(int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out);
+    int seed_splitmix(uint64_t seed);
+    int clear();
+    int place_points(const std::vector<int64_t>& xy);  // global (x, y) pairs, already wrapped
+    int step(int64_t generations, int64_t* done);      // *done: generations actually advanced
+    int reduce(bool hash, uint64_t* out);
+    int synchronize();
+
+    int parts() const { return (int)parts_.size(); }
+    const Part& part(int i) const { return parts_[(size_t)i]; }
+    int cur() const { return cur_; }
+    hipStream_t stream0() const { return parts_.empty() ? nullptr : parts_[0].compute; }
+    int max_k() const { return max_k_; }
+
+   private:
+    int pass(int k);
+    std::vector<Part> parts_;
+    int64_t W_ = 0, H_ = 0;
+    int boundary_ = GOL_TORUS, ilv_ = 1, tblock_ = 1, max_k_ = 1;
+    int cur_ = 0;
+};
+
+}  // namespace gol

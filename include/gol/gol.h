@@ -47,7 +47,11 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  * neighbour wiring (L21-30).  width/height >= 3 (smaller tori alias neighbours: the reference's
  * Dictionary never reaches 8 keys and the board freezes, GameOfLifeLogic.fs:58 -- rejected here).
  * boundary: GOL_TORUS (actors, GameOfLifeDriver.fs:25) or GOL_BOUNDED (Script.fsx:11).
- * num_gpus: must be 1 in this build (multi-GPU runs use one process per GPU, gol_strip_*).
+ * num_gpus: 1 = one board on the calling thread's current device.  N > 1 = row strips on devices
+ *           0..N-1 of THIS process (the reference host is one process, GameOfLifeDriver.fs:13-41): strip r
+ *           owns rows [H*r/N, H*(r+1)/N); every pass copies k halo rows between neighbouring strips
+ *           (hipMemcpyPeerAsync over xGMI) while the interior rows compute.  Needs width % 32 == 0.
+ *           Bit-identical to num_gpus = 1.  (One process per GPU instead: gol_strip_* below.)
  * tblock_k: upper bound on the generations fused per kernel pass (0 = the layout's default; else one of
  *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
  * The initial board is all dead. */
@@ -56,6 +60,14 @@ int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tb
  * interleaved block (width must be a multiple of 32*ilv). */
 int gol_create_ex(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, int ilv,
                   gol_board** out);
+/* As gol_create_ex with num_gpus = ndevices and strip r placed on devices[r] (a device may repeat, e.g.
+ * to run the multi-strip protocol on one GPU). */
+int gol_create_multi(int64_t width, int64_t height, int boundary, const int* devices, int ndevices, int tblock_k,
+                     int ilv, gol_board** out);
+/* Row strips of a board (1 unless created with num_gpus > 1) and where strip `part` lives: its device,
+ * first global row, owned rows and halo depth (ghost rows per side; 0 for a single board). */
+int gol_num_parts(gol_board* b, int* n);
+int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* rows, int64_t* ghost);
 int gol_destroy(gol_board* b);
 
 /* Board I/O: cells[x + y*width], len == width*height.  Replaces createCell's `alive` argument
@@ -101,7 +113,8 @@ int gol_supported_k(int k, int ilv);
  * the number of waves in a full-row workgroup (the row's blocks spread over one workgroup, block edges
  * exchanged through LDS), or 0 for per-wave column strips. */
 int gol_fullrow_wg(int64_t width, int ilv, int k);
-/* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller. */
+/* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller (multi-GPU
+ * boards: strip 0's compute stream, which every pass joins at its end). */
 int gol_stream(gol_board* b, void** stream);
 
 const char* gol_last_error(void);

@@ -71,8 +71,16 @@ void applyGrid(F&& f, Grid g = grid) {           // L13-15: x outer, y inner
 // ---------------------------------------------------------------- the board (replaces the cell agents)
 class Board {
    public:
-    Board(int64_t width, int64_t height, int boundary = GOL_TORUS, int tblock_k = 0) : w_(width), h_(height) {
-        check(gol_create(width, height, boundary, 1, tblock_k, &b_), "gol_create");
+    // num_gpus > 1: row strips over devices 0..num_gpus-1 of this process (gol.h gol_create)
+    Board(int64_t width, int64_t height, int boundary = GOL_TORUS, int tblock_k = 0, int num_gpus = 1)
+        : w_(width), h_(height) {
+        check(gol_create(width, height, boundary, num_gpus, tblock_k, &b_), "gol_create");
+    }
+    // explicit strip placement (gol_create_multi), e.g. {0, 0} runs two strips on one GPU
+    Board(int64_t width, int64_t height, int boundary, int tblock_k, const std::vector<int>& devices)
+        : w_(width), h_(height) {
+        check(gol_create_multi(width, height, boundary, devices.data(), (int)devices.size(), tblock_k, 0, &b_),
+              "gol_create_multi");
     }
     ~Board() {
         if (b_) gol_destroy(b_);

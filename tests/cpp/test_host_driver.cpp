@@ -84,6 +84,21 @@ static void gpu_tests() {
         CHECK(agent.frames() == n);  // no tick after Dispose
         delete game;
     }
+    // one board over row strips (gol_create_multi): devices {0, 0, 0} here, 0..n-1 on a multi-GPU node
+    {
+        const int w = 128, h = 96;
+        std::vector<uint8_t> a((size_t)(w * h)), b2(a.size()), px(a.size());
+        oracle_seed_dotnet(a.data(), w, h, 42, GOL_INIT_DOTNET_MOD2);
+        for (int i = 0; i < 20; i++) {
+            oracle_step(a.data(), b2.data(), w, h, GOL_TORUS);
+            a.swap(b2);
+        }
+        oracle_render_gray8(a.data(), w, h, px.data(), w, 128);
+        Board mb(w, h, GOL_TORUS, 0, std::vector<int>{0, 0, 0});
+        mb.seedDotnet(42).step(20);
+        CHECK(mb.renderGray8(128) == px);
+        CHECK(mb.generation() == 20);
+    }
     // error behaviour: invalid geometry throws with the library's code and message
     {
         bool threw = false;

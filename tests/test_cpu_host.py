@@ -93,6 +93,10 @@ def test_create_fails_loudly_without_gpu():
 
     with pytest.raises(RuntimeError):
         Board(64, 64)
+    with pytest.raises(RuntimeError):  # the multi-GPU board fails the same way (GOL_ERR_NO_DEVICE)
+        Board(64, 64, num_gpus=2)
+    with pytest.raises(RuntimeError):
+        Board(64, 64, devices=[0, 0])
 
 
 def test_invalid_arguments_rejected_before_device():
@@ -102,8 +106,12 @@ def test_invalid_arguments_rejected_before_device():
         Board(2, 100)  # < 3: the reference's Dictionary never reaches 8 keys (GameOfLifeLogic.fs:58)
     with pytest.raises(ValueError):
         Board(64, 64, boundary=7)
-    with pytest.raises(NotImplementedError):
-        Board(64, 64, num_gpus=2)
+    with pytest.raises(ValueError):
+        Board(64, 64, num_gpus=0)
+    with pytest.raises(ValueError):
+        Board(64, 64, num_gpus=65)
+    with pytest.raises(ValueError):
+        Board(64, 64, devices=[])
     with pytest.raises(ValueError):
         Board(64, 64, tblock_k=5)
 
