@@ -153,6 +153,28 @@ int pick_ilv(int64_t width) {
 // Default generations per pass for a layout (measured on MI355X, DESIGN.md "Temporal block depth").
 int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 32); }
 
+// Boards below this many cells are latency-bound, not throughput-bound: too few rows per wave to fill the
+// device, so a deep pass is one long serial chain per wave.  They get narrow strips (ilv 1) and a shallow
+// block (K = 8): 4096^2 8.8k vs 3.8k GCUPS at the large-board default (ilv 2, K = 12), 1024^2 554 vs 240,
+// 256^2 bounded 21.7 vs 13.3 (profiles/r1/small_sweep.log).
+constexpr int64_t kSmallBoardCells = (int64_t)1 << 25;
+// Mid-size boards (up to 2^29 cells) run one level deeper at ilv 2: 16384^2 K = 16 56.1k vs K = 12 54.1k.
+constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
+
+// Layout and depth a new board gets when the caller leaves them at 0.
+int board_ilv(int64_t width, int64_t height) {
+    const int env = pick_ilv(width);
+    if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) return 1;
+    return env;
+}
+int board_tblock(int ilv, int64_t cells, int boundary, int parts) {
+    if (ilv == 1 && cells < kSmallBoardCells) return 8;
+    // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log);
+    // ghost-row strips (multi-GPU) likewise (K = 16 105k vs K = 12 97k GCUPS, profiles/r1/ghost_ab2.log)
+    if (ilv == 2 && (boundary == GOL_BOUNDED || parts > 1 || cells < kMidBoardCells)) return 16;
+    return default_tblock(ilv);
+}
+
 }  // namespace
 
 namespace gol {
@@ -403,11 +425,8 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->boundary = boundary;
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
-        b->ilv = b->packed ? (ilv ? ilv : pick_ilv(width)) : 0;
-        // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log);
-        // ghost-row strips (multi-GPU) likewise (K = 16 105k vs K = 12 97k GCUPS, profiles/r1/ghost_ab2.log)
-        b->tblock = tblock_k ? tblock_k
-                             : ((boundary == GOL_BOUNDED || n > 1) && b->ilv == 2 ? 16 : default_tblock(b->ilv));
+        b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height)) : 0;
+        b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary, n);
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = devices ? hipSetDevice(devices[0]) : hipSuccess;
         if (e == hipSuccess) e = hipGetDevice(&b->device);

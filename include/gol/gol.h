@@ -52,8 +52,10 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *           owns rows [H*r/N, H*(r+1)/N); every pass copies k halo rows between neighbouring strips
  *           (hipMemcpyPeerAsync over xGMI) while the interior rows compute.  Needs width % 32 == 0.
  *           Bit-identical to num_gpus = 1.  (One process per GPU instead: gol_strip_* below.)
- * tblock_k: upper bound on the generations fused per kernel pass (0 = the layout's default; else one of
- *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
+ * tblock_k: upper bound on the generations fused per kernel pass (0 = the engine's default for the
+ *           board: latency-bound boards below 2^25 cells get ilv 1 and k = 8; larger ones ilv 2 and k = 16,
+ *           k = 12 from 2^29 cells on a single torus; else one of 1,2,4,6,8,12,16,24,32 -- the engine uses
+ *           the deepest supported depth <= tblock_k).  gol_layout / gol_info report the choice.
  * The initial board is all dead. */
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
 /* As gol_create with an explicit packed layout: ilv = 0 (auto, gol_default_ilv) or 1, 2, 4 words per
@@ -104,8 +106,9 @@ int gol_hash(gol_board* b, uint64_t* out); /* canonical 64-bit board hash (DESIG
 int gol_info(gol_board* b, int64_t* width, int64_t* height, int* boundary, int* tblock_k, int* packed);
 /* Packed layout of the board: ilv = words per interleaved block (1, 2, 4; 0 = byte board), pitch in words. */
 int gol_layout(gol_board* b, int* ilv, int64_t* pitch);
-/* Layout / depth the engine picks for a width (0 if the width is not a multiple of 32), the default
- * temporal-block depth for a layout, and whether the step kernel supports depth k for a layout. */
+/* Layout / depth the engine picks for a large board of this width (0 if the width is not a multiple of
+ * 32; boards below 2^25 cells use ilv 1, see gol_create), the default temporal-block depth for a layout
+ * on a large board, and whether the step kernel supports depth k for a layout. */
 int gol_default_ilv(int64_t width);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
