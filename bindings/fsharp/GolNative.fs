@@ -28,6 +28,10 @@ extern int gol_step(nativeint board, int64 generations)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gol_render_gray8(nativeint board, byte[] pixels, int64 stride, byte aliveValue)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_save_packed(nativeint board, uint64[] words, int64 len)   // canonical snapshot, H*ceil(W/64)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_load_packed(nativeint board, uint64[] words, int64 len)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gol_population(nativeint board, int64& out)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gol_hash(nativeint board, uint64& out)
@@ -50,5 +54,9 @@ type Board(width: int, height: int, boundary: Boundary, ?numGpus: int) =
         check "gol_get_cells" (gol_get_cells(h, a, int64 a.Length)); a
     member _.Render(pixels: byte[], alive: byte) =
         check "gol_render_gray8" (gol_render_gray8(h, pixels, int64 width, alive))
+    member _.Save() =   // 1 bit per cell, layout- and GPU-count-independent
+        let w = Array.zeroCreate<uint64> (height * ((width + 63) / 64))
+        check "gol_save_packed" (gol_save_packed(h, w, int64 w.Length)); w
+    member _.Load(words: uint64[]) = check "gol_load_packed" (gol_load_packed(h, words, int64 words.Length))
     interface IDisposable with
         member _.Dispose() = if h <> 0n then (gol_destroy h |> ignore; h <- 0n)

@@ -79,6 +79,8 @@ SIGNATURES = {
     "gol_get_region": (ctypes.c_int, [vp, i64, i64, i64, i64, u8p]),
     "gol_seed_dotnet": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int]),
     "gol_seed_splitmix": (ctypes.c_int, [vp, u64]),
+    "gol_save_packed": (ctypes.c_int, [vp, u64p, i64]),
+    "gol_load_packed": (ctypes.c_int, [vp, u64p, i64]),
     "gol_place_rle": (ctypes.c_int, [vp, ctypes.c_char_p, i64, i64]),
     "gol_clear": (ctypes.c_int, [vp]),
     "gol_step": (ctypes.c_int, [vp, i64]),

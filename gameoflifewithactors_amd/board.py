@@ -12,7 +12,7 @@ import ctypes
 
 import numpy as np
 
-from . import _lib
+from . import _lib, patterns
 from ._lib import BOUNDED, INIT_DOTNET_MOD2, INIT_DOTNET_NEXT2, TORUS, check
 
 __all__ = ["Board", "TORUS", "BOUNDED", "INIT_DOTNET_MOD2", "INIT_DOTNET_NEXT2", "hash_finalize"]
@@ -97,6 +97,42 @@ class Board:
     def seed_dotnet(self, seed: int, mode: int = INIT_DOTNET_MOD2) -> "Board":
         check(self._lib.gol_seed_dotnet(self._h, seed, mode), "gol_seed_dotnet")
         return self
+
+    # ---------------------------------------------------------------- snapshots and patterns
+    def save_packed(self) -> np.ndarray:
+        """Canonical bit-packed snapshot (gol_save_packed): (height, ceil(width/64)) uint64."""
+        nc = (self.width + 63) // 64
+        out = np.empty((self.height, nc), dtype="<u8")
+        check(self._lib.gol_save_packed(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), out.size),
+              "gol_save_packed")
+        return out
+
+    def load_packed(self, words) -> "Board":
+        a = np.ascontiguousarray(np.asarray(words, dtype="<u8")).reshape(-1)
+        check(self._lib.gol_load_packed(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), a.size),
+              "gol_load_packed")
+        return self
+
+    def save(self, path: str) -> None:
+        """Write a snapshot file (patterns.write_snapshot): header + canonical rows, 1 bit per cell."""
+        patterns.write_snapshot(path, self.save_packed(), self.width, self.height, self.boundary, self.generation,
+                                self.hash())
+
+    @classmethod
+    def from_snapshot(cls, path: str, **kw) -> "Board":
+        """A new board holding a snapshot file's cells (same size and boundary); the canonical hash recorded
+        in the file is checked after the upload.  kw: tblock_k, num_gpus, ilv, devices."""
+        head, words = patterns.read_snapshot(path)
+        b = cls(head["width"], head["height"], head["boundary"], **kw)
+        b.load_packed(words)
+        if b.hash() != head["hash"]:
+            b.close()
+            raise ValueError(f"{path}: board hash after load differs from the snapshot's")
+        return b
+
+    def to_rle(self) -> str:
+        """The board as RLE text (patterns.to_rle); place it back with place_rle(text, 0, 0)."""
+        return patterns.to_rle(self.get_cells())
 
     def seed_splitmix(self, seed: int) -> "Board":
         check(self._lib.gol_seed_splitmix(self._h, seed & 0xFFFFFFFFFFFFFFFF), "gol_seed_splitmix")

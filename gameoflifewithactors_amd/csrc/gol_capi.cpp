@@ -593,6 +593,55 @@ int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t aliv
     return readback_impl(b, pixels, stride, alive_value);
 }
 
+int gol_save_packed(gol_board* b, uint64_t* words, int64_t len) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
+    const int64_t nc = (b->W + 63) / 64;
+    if (!words || len != nc * b->H) return fail(GOL_ERR_INVALID, "words length must be height * ceil(width/64)");
+    if (b->multi) return b->multi->save_packed(words);
+    const size_t n = (size_t)len * 8;
+    uint64_t* staging = nullptr;
+    hipError_t e = hipMalloc(&staging, n);
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc snapshot");
+    do {
+        e = gol::launch_export_canonical(b->buf[b->cur], b->W, b->H, b->pitch, 0, b->packed ? b->ilv : 0, staging,
+                                         b->stream);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(words, staging, n, hipMemcpyDeviceToHost, b->stream);
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    (void)hipFree(staging);
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("save_packed: ") + hipGetErrorString(e));
+    return GOL_OK;
+}
+
+int gol_load_packed(gol_board* b, const uint64_t* words, int64_t len) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
+    const int64_t nc = (b->W + 63) / 64;
+    if (!words || len != nc * b->H) return fail(GOL_ERR_INVALID, "words length must be height * ceil(width/64)");
+    b->generation = 0;
+    if (b->multi) return b->multi->load_packed(words);
+    const size_t n = (size_t)len * 8;
+    uint64_t* staging = nullptr;
+    hipError_t e = hipMalloc(&staging, n);
+    if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc snapshot");
+    do {
+        e = hipMemcpyAsync(staging, words, n, hipMemcpyHostToDevice, b->stream);
+        if (e != hipSuccess) break;
+        e = gol::launch_import_canonical(staging, b->W, b->H, b->pitch, 0, b->packed ? b->ilv : 0, b->buf[b->cur],
+                                         b->stream);
+        if (e != hipSuccess) break;
+        e = hipStreamSynchronize(b->stream);
+    } while (0);
+    (void)hipFree(staging);
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("load_packed: ") + hipGetErrorString(e));
+    return GOL_OK;
+}
+
 int gol_seed_dotnet(gol_board* b, int32_t seed, int mode) {
     if (int rc = check_board(b)) return rc;
     std::lock_guard<std::mutex> g(b->mu);

@@ -159,6 +159,24 @@ __global__ void gol_popcount_bytes(const uint8_t* __restrict__ cells, int64_t n,
     if ((threadIdx.x & 63) == 0 && sum) atomicAdd(acc, (unsigned long long)sum);
 }
 
+// Canonical 64-cell chunk j of a packed row r (layout ilv): bit i = cell 64j + i, zero past the width.
+// The layout-independent form behind the hash and the board snapshot (gol_save_packed).
+__device__ __forceinline__ uint64_t canonical_chunk(const uint32_t* r, int64_t W, int64_t j, int ilv) {
+    if (ilv == 1) {
+        const uint64_t lo = r[2 * j];
+        const uint64_t hi = (2 * j + 1 < W / 32) ? r[2 * j + 1] : 0u;
+        return lo | (hi << 32);
+    }
+    uint64_t v = 0;
+    for (int i = 0; i < 64 && 64 * j + i < W; i++) {
+        int64_t word;
+        int bit;
+        cell_pos(64 * j + i, ilv, word, bit);
+        v |= (uint64_t)((r[word] >> bit) & 1u) << i;
+    }
+    return v;
+}
+
 // Canonical hash partial sum: for 64-cell chunk j of global row gy, v bit i = cell 64j + i;
 // sum += fmix64(v ^ fmix64(gy * ceil(W/64) + j + phi)).  One thread per chunk.
 __global__ void gol_hash_packed(const uint32_t* __restrict__ words, int64_t W, int64_t rows, int64_t pitch,
@@ -168,20 +186,7 @@ __global__ void gol_hash_packed(const uint32_t* __restrict__ words, int64_t W, i
     uint64_t sum = 0;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t j = idx % nc, y = idx / nc;
-        const uint32_t* r = words + (row0 + y) * pitch;
-        uint64_t v = 0;
-        if (ilv == 1) {
-            const uint64_t lo = r[2 * j];
-            const uint64_t hi = (2 * j + 1 < W / 32) ? r[2 * j + 1] : 0u;
-            v = lo | (hi << 32);
-        } else {
-            for (int i = 0; i < 64 && 64 * j + i < W; i++) {
-                int64_t word;
-                int bit;
-                cell_pos(64 * j + i, ilv, word, bit);
-                v |= (uint64_t)((r[word] >> bit) & 1u) << i;
-            }
-        }
+        const uint64_t v = canonical_chunk(words + (row0 + y) * pitch, W, j, ilv);
         const uint64_t key = (uint64_t)((gy0 + y) * nc + j);
         sum += fmix64(v ^ fmix64(key + 0x9E3779B97F4A7C15ULL));
     }
@@ -215,6 +220,47 @@ __global__ void gol_set_points(void* board, int ilv, int64_t W, int64_t pitch, c
         atomicOr(&static_cast<uint32_t*>(board)[y * pitch + word], 1u << bit);
     } else {
         static_cast<uint8_t*>(board)[x + y * W] = 1;
+    }
+}
+
+// Board snapshot (gol_save_packed / gol_load_packed): canonical chunks out[y * ceil(W/64) + j].
+// ilv > 0: packed board rows at buffer row row0 + y; ilv = 0: byte board (cells[x + y*W]).
+__global__ void gol_export_canonical(const void* __restrict__ board, int64_t W, int64_t rows, int64_t pitch,
+                                     int64_t row0, int ilv, uint64_t* __restrict__ out) {
+    const int64_t nc = (W + 63) / 64;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nc * rows) return;
+    const int64_t j = idx % nc, y = idx / nc;
+    uint64_t v = 0;
+    if (ilv > 0) {
+        v = canonical_chunk(static_cast<const uint32_t*>(board) + (row0 + y) * pitch, W, j, ilv);
+    } else {
+        const uint8_t* c = static_cast<const uint8_t*>(board) + y * W;
+        for (int b = 0; b < 64 && j * 64 + b < W; b++) v |= (uint64_t)(c[j * 64 + b] != 0) << b;
+    }
+    out[idx] = v;
+}
+
+// inverse: one thread per stored word (packed) or per cell (bytes); bits past the width are ignored
+__global__ void gol_import_canonical(const uint64_t* __restrict__ in, int64_t W, int64_t rows, int64_t pitch,
+                                     int64_t row0, int ilv, void* __restrict__ board) {
+    const int64_t nc = (W + 63) / 64;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ilv > 0) {
+        const int64_t wpr = W / 32;
+        if (idx >= wpr * rows) return;
+        const int64_t w = idx % wpr, y = idx / wpr;
+        const uint64_t* r = in + y * nc;
+        uint32_t v = 0;
+        for (int b = 0; b < 32; b++) {
+            const int64_t x = word_bit_cell(w, b, ilv);
+            v |= (uint32_t)((r[x >> 6] >> (x & 63)) & 1u) << b;
+        }
+        static_cast<uint32_t*>(board)[(row0 + y) * pitch + w] = v;
+    } else {
+        if (idx >= W * rows) return;
+        const int64_t x = idx % W, y = idx / W;
+        static_cast<uint8_t*>(board)[idx] = (uint8_t)((in[y * nc + (x >> 6)] >> (x & 63)) & 1u);
     }
 }
 
@@ -297,6 +343,20 @@ hipError_t launch_hash_packed(const uint32_t* words, int64_t W, int64_t rows, in
 
 hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s) {
     hipLaunchKernelGGL(gol_hash_bytes, dim3(grid_stride((W + 63) / 64 * H)), dim3(256), 0, s, cells, W, H, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_canonical(const void* board, int64_t W, int64_t rows, int64_t pitch, int64_t row0, int ilv,
+                                   uint64_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(gol_export_canonical, dim3(grid1d((W + 63) / 64 * rows)), dim3(256), 0, s, board, W, rows, pitch,
+                       row0, ilv, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_import_canonical(const uint64_t* in, int64_t W, int64_t rows, int64_t pitch, int64_t row0, int ilv,
+                                   void* board, hipStream_t s) {
+    const int64_t n = ilv > 0 ? W / 32 * rows : W * rows;
+    hipLaunchKernelGGL(gol_import_canonical, dim3(grid1d(n)), dim3(256), 0, s, in, W, rows, pitch, row0, ilv, board);
     return hipGetLastError();
 }
 

@@ -57,6 +57,11 @@ hipError_t launch_popcount_bytes(const uint8_t* cells, int64_t n, unsigned long 
 hipError_t launch_hash_packed(const uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                               int64_t gy0, int ilv, unsigned long long* acc, hipStream_t s);
 hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s);
+// canonical snapshot rows (ceil(W/64) uint64 per row); ilv = 0: byte board
+hipError_t launch_export_canonical(const void* board, int64_t W, int64_t rows, int64_t pitch, int64_t row0, int ilv,
+                                   uint64_t* out, hipStream_t s);
+hipError_t launch_import_canonical(const uint64_t* in, int64_t W, int64_t rows, int64_t pitch, int64_t row0, int ilv,
+                                   void* board, hipStream_t s);
 hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, const int64_t* xy, int64_t n,
                              hipStream_t s);
 

@@ -176,6 +176,36 @@ int MultiBoard::region(int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out)
     return GOL_OK;
 }
 
+int MultiBoard::save_packed(uint64_t* host) {
+    const int64_t nc = (W_ + 63) / 64;
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t n = (size_t)(p.s.rows * nc) * 8;
+        Staging st;
+        GOL_MRC(st.alloc(n));
+        GOL_MHIP(launch_export_canonical(p.buf[cur_], W_, p.s.rows, p.s.pitch, p.s.ghost, ilv_,
+                                         static_cast<uint64_t*>(st.p), p.compute));
+        GOL_MHIP(hipMemcpyAsync(host + p.s.y0 * nc, st.p, n, hipMemcpyDeviceToHost, p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::load_packed(const uint64_t* host) {
+    const int64_t nc = (W_ + 63) / 64;
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        const size_t n = (size_t)(p.s.rows * nc) * 8;
+        Staging st;
+        GOL_MRC(st.alloc(n));
+        GOL_MHIP(hipMemcpyAsync(st.p, host + p.s.y0 * nc, n, hipMemcpyHostToDevice, p.compute));
+        GOL_MHIP(launch_import_canonical(static_cast<const uint64_t*>(st.p), W_, p.s.rows, p.s.pitch, p.s.ghost, ilv_,
+                                         p.buf[cur_], p.compute));
+        GOL_MHIP(hipStreamSynchronize(p.compute));
+    }
+    return GOL_OK;
+}
+
 int MultiBoard::seed_splitmix(uint64_t seed) {
     for (Part& p : parts_) {
         GOL_MHIP(hipSetDevice(p.device));

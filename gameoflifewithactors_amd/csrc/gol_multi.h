@@ -41,6 +41,8 @@ class MultiBoard {
     int readback(uint8_t* host, int64_t stride, uint8_t value);
     int region(int64_t x, int64_t y, int64_t w, int64_t h, uint8_t* out);
     int seed_splitmix(uint64_t seed);
+    int save_packed(uint64_t* host);        // canonical snapshot rows (gol_save_packed)
+    int load_packed(const uint64_t* host);
     int clear();
     int place_points(const std::vector<int64_t>& xy);  // global (x, y) pairs, already wrapped
     int step(int64_t generations, int64_t* done);      // *done: generations actually advanced

@@ -84,6 +84,13 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
  * the build-owned device-side init for large boards.  gol_place_rle ORs a Life RLE pattern
  * with its top-left at (x, y), wrapped modulo the board. */
 int gol_seed_dotnet(gol_board* b, int32_t seed, int mode);
+/* Board snapshot (save / restore, SURVEY 8f "board save/load") in the canonical bit-packed layout the
+ * hash is defined on, independent of the board's internal layout and GPU count: row y is ceil(width/64)
+ * little-endian uint64 words, bit i of word j = cell (64j + i, y), bits past the width zero;
+ * len = height * ceil(width/64).  A snapshot taken from any board loads into any board of the same size.
+ * gol_load_packed resets the generation counter (like gol_set_cells). */
+int gol_save_packed(gol_board* b, uint64_t* words, int64_t len);
+int gol_load_packed(gol_board* b, const uint64_t* words, int64_t len);
 int gol_seed_splitmix(gol_board* b, uint64_t seed);
 int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y);
 int gol_clear(gol_board* b);

@@ -52,14 +52,19 @@ def test_packed_step_matches_oracle(gol, oracle, boundary, ilv, w, h):
 
 
 @pytest.mark.parametrize("boundary", [0, 1])
-@pytest.mark.parametrize("w,h", [(3, 3), (100, 100), (33, 7), (257, 40)])
+@pytest.mark.parametrize("w,h", [(3, 3), (100, 100), (33, 7), (257, 40), (181, 181), (1001, 33), (333, 333)])
 def test_byte_path_matches_oracle(gol, oracle, boundary, w, h):
+    """Ragged widths (byte-per-cell board, one gol_bytes_step launch per generation), split step calls."""
     b0 = _rand(h, w, w + 7 * h)
     with gol.Board(w, h, boundary) as b:
         assert not b.info()["packed"]
         b.set_cells(b0)
         b.step(25)
         assert np.array_equal(b.get_cells(), oracle.c_run(b0, 25, boundary))
+        b.step(1)
+        b.step(4)
+        assert b.generation == 30
+        assert np.array_equal(b.get_cells(), oracle.c_run(b0, 30, boundary))
 
 
 @pytest.mark.parametrize("k", KS)
