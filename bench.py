@@ -226,6 +226,22 @@ def main():
               "avg_launch_us": round(t1 * 1e6, 2)}
         k1["frac"] = round(k1["achieved"] / HBM_PEAK_GBS, 4)
 
+    # Measured device-to-device copy rate on this box (torch copy_ of 1 GiB, 512 MiB read + 512 MiB written
+    # per copy), outside the timed region: the practical HBM ceiling the roofline fractions sit under.
+    copy_gbs = None
+    if world == 1:
+        a_ = torch.empty(1 << 27, dtype=torch.int32, device="cuda")
+        b_ = torch.empty_like(a_)
+        b_.copy_(a_)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(10):
+            b_.copy_(a_)
+        c1.record()
+        torch.cuda.synchronize()
+        copy_gbs = round(2 * a_.numel() * 4 * 10 / (c0.elapsed_time(c1) / 1e3) / 1e9, 1)
+        del a_, b_
+
     cells = W * H
     gens = args.steps * k
     gcups = cells * gens / dt / 1e9
@@ -288,6 +304,7 @@ def main():
             },
             "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
             "roofline_k1_stream": k1,
+            "hbm_copy_measured_gbs": copy_gbs,
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure (rank 0 only)
             result["cpu_baseline"] = cpu_baseline(args)
