@@ -1,12 +1,13 @@
 """Benchmark: cell updates per second (GCUPS) of the hot path on MI355X, plus roofline and CPU baseline.
 
-Workload (BASELINE.json metric "GCUPS at 65536^2 on 1 and 8 x MI355X"): a 65536 x 65536 torus, splitmix
-random 50 % fill generated on the device (data: synthetic).  One *step* = one pass of the streaming
-kernel that advances the whole board by `tblock` generations (temporal blocking).  For N GPUs (one
+Workload (BASELINE.json metric "GCUPS at 65536^2 on 1 and 8 x MI355X", config 3 "65536^2 bit-packed
+board, 10k generations on one MI355X"): a 65536 x 65536 torus, splitmix random 50 % fill generated on the
+device (data: synthetic).  One *step* = one pass of the streaming kernel that advances the whole board by
+`tblock` generations (temporal blocking); by default the timed steps cover the whole 10k-generation job.  For N GPUs (one
 process per GPU under torchrun) the board is 65536 wide and 65536*N tall, split into N row strips of
 65536^2 cells with RCCL halo exchange (weak scaling: per-GPU work fixed).
 
-    python bench.py                          # N = 1, defaults finish in well under a minute
+    python bench.py                          # N = 1: 10k generations timed (~0.5 s), under a minute in all
     python bench.py --steps 64 --warmup 4 --tblock 16
     torchrun --nproc-per-node 8 bench.py --gpus 8
 
@@ -57,7 +58,10 @@ def valu_slots_per_word_gen(ilv: int) -> float:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--steps", type=int, default=0,
+                   help="timed passes (0 = enough passes for --generations: the whole BASELINE config-3 job)")
+    p.add_argument("--generations", type=int, default=10000,
+                   help="generations the default run times (BASELINE config 3: 65536^2, 10k generations)")
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--width", type=int, default=65536)
     p.add_argument("--height", type=int, default=65536, help="rows per GPU (board height = height * gpus)")
@@ -180,6 +184,8 @@ def main():
         k = cands[min(range(len(cands)), key=lambda i: per_gen[i])]
         tune = {str(kk): round(1e3 * pg, 3) for kk, pg in zip(cands, per_gen)}  # us per generation
     runner.k = k
+    if args.steps <= 0:  # the whole job: ceil(generations / k) passes of k generations
+        args.steps = -(-args.generations // k)
 
     for _ in range(args.warmup):
         runner.step_pass()
@@ -271,11 +277,12 @@ def main():
             "dtype": "u32 (bit-packed cells)",
             "data": "synthetic (splitmix 50% fill generated on device)",
             "config": {
-                "workload": f"{W}x{H} {args.boundary} board, {k} generations per step (temporal block), "
-                f"{world} row strip(s)",
+                "workload": f"{W}x{H} {args.boundary} board, {args.steps * k} generations timed in passes of "
+                f"{k} (temporal block), {world} row strip(s)",
                 "width": W,
                 "height": H,
                 "generations_per_step": k,
+                "generations_timed": args.steps * k,
                 "tblock_autotune_us_per_gen": tune,
                 "interleave": ilv,
                 "boundary": args.boundary,
