@@ -33,11 +33,12 @@ AUTOTUNE = {2: [12, 16], 1: [24, 32]}
 
 def default_depth(lib, ilv: int, world: int, boundary: str) -> int:
     """Fixed default temporal depth, so the bench line and a rocprof trace of the same command run the same
-    kernel.  Single board (rows wrap in the buffer): the engine default (K = 12 at M = 2: 104.7-110.7k vs
-    99-106k GCUPS for K = 16, profiles/r1/w12_sweep*.log, bench_session3.log).  Ghost-row strips (N > 1):
-    K = 16 (105.1k vs 96.8k for K = 12, profiles/r1/ghost_ab2.log).  Bounded boards at M = 2 keep 8-wave
-    workgroups, where K = 16 is faster (78.5k vs 74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
-    if ilv == 2 and (world > 1 or boundary == "bounded"):
+    kernel.  Torus, single board or ghost-row strips (N > 1): the engine default K = 12 at M = 2 (12-wave
+    workgroups).  Over the whole 10k-generation job it beats K = 16 on both: single board 116.4k vs 109.5k
+    GCUPS (profiles/r1/bench_k_ab.log), strips 113.7-114.1k vs 99.2-101.0k (strip_k_ab.log); K = 16 wins only
+    on the first passes of a fresh board (ghost_ab2.log).  Bounded boards at M = 2 keep 8-wave workgroups,
+    where K = 16 is faster (78.5k vs 74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
+    if ilv == 2 and boundary == "bounded":
         return 16
     return int(lib.gol_default_tblock(ilv))
 

@@ -169,9 +169,11 @@ int board_ilv(int64_t width, int64_t height) {
 }
 int board_tblock(int ilv, int64_t cells, int boundary, int parts) {
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
-    // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log);
-    // ghost-row strips (multi-GPU) likewise (K = 16 105k vs K = 12 97k GCUPS, profiles/r1/ghost_ab2.log)
-    if (ilv == 2 && (boundary == GOL_BOUNDED || parts > 1 || cells < kMidBoardCells)) return 16;
+    // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log).
+    // Ghost-row strips (multi-GPU) keep K = 12: over a whole 10k-generation job 114k vs 100k GCUPS for
+    // K = 16 (profiles/r1/strip_k_ab.log), although K = 16 leads on a fresh board's first passes.
+    (void)parts;
+    if (ilv == 2 && (boundary == GOL_BOUNDED || cells < kMidBoardCells)) return 16;
     return default_tblock(ilv);
 }
 

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--size", type=int, default=65536)
     p.add_argument("--parts", default="1,2,4,8")
     p.add_argument("--passes", type=int, default=16)
+    p.add_argument("--generations", type=int, default=0, help="time this many generations instead of --passes")
     p.add_argument("--tblock", type=int, default=0)
     p.add_argument("--weak", action="store_true", help="board height = size * parts (each strip size x size)")
     p.add_argument("--devices", default="", help="comma list of devices per part (default: all on device 0)")
@@ -38,6 +39,8 @@ def main():
             b.seed_splitmix(0x5EED)
             b.step(2 * k)
             b.synchronize()
+            if a.generations:
+                a.passes = -(-a.generations // k)
             t0 = time.perf_counter()
             b.step(a.passes * k)
             b.synchronize()
