@@ -147,3 +147,30 @@ def test_262144_board_strips_match_single_board():
     del lb
     torch.cuda.empty_cache()
     assert got_hash == want[0]
+
+
+def test_bench_single_gpu_json_contract():
+    """bench.py at N = 1: one JSON line with the driver's keys, the roofline object (achieved / peak =
+    frac) and the CPU actor baseline (short sample here)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "4", "--warmup", "1", "--height", "8192",
+           "--cpu-seconds", "1", "--cpu-board", "64"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in r, key
+    assert r["n_gpus"] == 1 and r["steps"] == 4 and r["warmup"] == 1 and r["value"] > 0
+    assert r["higher_is_better"] is True and r["vs_baseline"] is None and "workload" in r["config"]
+    rf = r["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cb = r["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["unit"] == "GCUPS" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
