@@ -167,12 +167,11 @@ int board_ilv(int64_t width, int64_t height) {
     if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) return 1;
     return env;
 }
-int board_tblock(int ilv, int64_t cells, int boundary, int parts) {
+int board_tblock(int ilv, int64_t cells, int boundary) {
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
     // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log).
     // Ghost-row strips (multi-GPU) keep K = 12: over a whole 10k-generation job 114k vs 100k GCUPS for
     // K = 16 (profiles/r1/strip_k_ab.log), although K = 16 leads on a fresh board's first passes.
-    (void)parts;
     if (ilv == 2 && (boundary == GOL_BOUNDED || cells < kMidBoardCells)) return 16;
     return default_tblock(ilv);
 }
@@ -428,7 +427,7 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height)) : 0;
-        b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary, n);
+        b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = devices ? hipSetDevice(devices[0]) : hipSuccess;
         if (e == hipSuccess) e = hipGetDevice(&b->device);
