@@ -860,7 +860,12 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         const int64_t slots = units / group;
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
-        const int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * group;
+        int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * group;
+        // A launch too small to fill a quarter of the device is latency-bound: each wave is one serial
+        // chain of (segment + 2k) rows x k levels, so shorter segments (more, shorter chains) finish sooner
+        // despite the extra pipeline fill.  1024^2: 549 -> 696 GCUPS, 4096^2: 8.7k -> 10.5k at K = 8, ilv 1
+        // (profiles/r1/small_seg.log).  Large boards are bounded by `slots` below and do not change.
+        if ((rows / min_seg) * a.nstrips * group < units / 4) min_seg = (k > 8 ? k : 8) * group;
         const int64_t max_segs = rows / min_seg > 0 ? rows / min_seg : 1;
         if (nsegs > max_segs) nsegs = max_segs;
         seg = (rows + nsegs - 1) / nsegs;
