@@ -54,8 +54,9 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *           Bit-identical to num_gpus = 1.  (One process per GPU instead: gol_strip_* below.)
  * tblock_k: upper bound on the generations fused per kernel pass (0 = the engine's default for the
  *           board: latency-bound boards below 2^25 cells get ilv 1 and k = 8; larger ones ilv 2 and k = 16,
- *           k = 12 from 2^29 cells on a single torus; else one of 1,2,4,6,8,12,16,24,32 -- the engine uses
- *           the deepest supported depth <= tblock_k).  gol_layout / gol_info report the choice.
+ *           k = 12 from 2^29 cells on a torus (single GPU or strips); bounded boards k = 16; else one of
+ *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
+ *           gol_layout / gol_info report the choice.
  * The initial board is all dead. */
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
 /* As gol_create with an explicit packed layout: ilv = 0 (auto, gol_default_ilv) or 1, 2, 4 words per
