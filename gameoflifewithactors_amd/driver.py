@@ -114,14 +114,16 @@ def run(
     period_s: Optional[float] = None,
     emit: str = "updates",
     tblock_k: int = 0,
+    num_gpus: int = 1,
 ) -> GameOfLife:
     """GameOfLifeDriver.fs:13-41.  ``seed`` replaces ``int DateTime.Now.Ticks`` (L10) so runs are
     reproducible; the board is seeded x outer / y inner with ``Random.Next() % 2 = 0`` (L9-11,16-19).
-    With ``period_s`` a timer ticks like L38-40 (reference: ProcessorCount * 70 ms)."""
+    With ``period_s`` a timer ticks like L38-40 (reference: ProcessorCount * 70 ms).  ``num_gpus`` > 1
+    spreads the board over that many GPUs of this process (row strips; needs a width divisible by 32)."""
     if seed is None:
         seed = int(time.time_ns() // 100) & 0xFFFFFFFF  # .NET ticks are 100 ns; `int` truncates to 32 bits
         seed = seed - (1 << 32) if seed >= (1 << 31) else seed
-    board = Board(g.Width, g.Height, boundary, tblock_k)
+    board = Board(g.Width, g.Height, boundary, tblock_k, num_gpus=num_gpus)
     board.seed_dotnet(seed, INIT_DOTNET_MOD2)
     game = GameOfLife(board, agent or UpdateAgent(g), emit)
     if period_s is not None:
