@@ -160,6 +160,11 @@ int default_tblock(int ilv) { return ilv == 4 ? 8 : (ilv == 2 ? 12 : 32); }
 constexpr int64_t kSmallBoardCells = (int64_t)1 << 25;
 // Mid-size boards (up to 2^29 cells) run one level deeper at ilv 2: 16384^2 K = 16 56.1k vs K = 12 54.1k.
 constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
+// LDS-resident pass (gol_resident.hip) cut-overs, measured on MI355X (profiles/r1/resident_small.log):
+// packed 256^2 0.91 vs 1.47 us/generation on the streaming pass, 512x256 1.23 vs 1.47, but 512^2 1.87 vs
+// 1.49; byte boards 100^2 2.10 vs 3.56, but 255x257 10.7 vs 3.4.
+constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
+constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
@@ -167,6 +172,15 @@ int board_ilv(int64_t width, int64_t height) {
     if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) return 1;
     return env;
 }
+// Boards up to this many cells run every gol_step call as ONE launch of the LDS-resident kernel
+// (gol_resident.hip) when the layout fits it: whole board in one workgroup's LDS, one barrier per
+// generation.  GOL_RESIDENT_MAX_CELLS overrides (0 disables; experiments and A/B runs).
+// Read on every call, so one process can A/B both paths (tests/test_gpu_resident.py).
+int64_t resident_max_cells(bool packed) {
+    const char* e = std::getenv("GOL_RESIDENT_MAX_CELLS");
+    return e ? (int64_t)std::atoll(e) : (packed ? kResidentMaxCells : kResidentBytesMaxCells);
+}
+
 int board_tblock(int ilv, int64_t cells, int boundary) {
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
     // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log).
@@ -306,6 +320,23 @@ int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
 
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
+    if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
+        (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
+        const bool bounded = b->boundary == GOL_BOUNDED;
+        while (gens > 0) {
+            const int64_t g = gens < INT32_MAX ? gens : INT32_MAX;
+            if (b->packed)
+                GOL_HIP(gol::launch_resident_packed(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, g,
+                                                    bounded, b->stream));
+            else
+                GOL_HIP(gol::launch_resident_bytes(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H, g, bounded,
+                                                   b->stream));
+            b->cur ^= 1;
+            b->generation += g;
+            gens -= g;
+        }
+        return GOL_OK;
+    }
     if (!b->packed) {
         for (int64_t g = 0; g < gens; g++) {
             GOL_HIP(gol::launch_bytes_step(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H,

@@ -65,4 +65,12 @@ hipError_t launch_import_canonical(const uint64_t* in, int64_t W, int64_t rows, 
 hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, const int64_t* xy, int64_t n,
                              hipStream_t s);
 
+// ---- gol_resident.hip: whole board in one workgroup's LDS, all generations in one launch
+bool resident_packed_fits(int64_t W, int64_t H);  // ilv = 1 layout
+bool resident_bytes_fits(int64_t W, int64_t H);
+hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch,
+                                  int64_t gens, bool bounded, hipStream_t s);
+hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, int64_t gens, bool bounded,
+                                 hipStream_t s);
+
 }  // namespace gol

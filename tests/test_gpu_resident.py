@@ -1,0 +1,78 @@
+"""GPU parity of the LDS-resident small-board pass (csrc/gol_resident.hip).
+
+Boards up to 2^17 cells (packed ilv 1) or 2^14 cells (byte layout, widths not a multiple of 32) run a whole
+gol_step call as one launch with the board held in one workgroup's LDS by default; the kernel itself takes
+up to 2^19 / 2^16 cells, which these tests reach with GOL_RESIDENT_MAX_CELLS raised.  Bar: bit-exact against the oracle
+(GameOfLifeLogic.fs:56-63 rule, torus GameOfLifeDriver.fs:21-25, bounded Script.fsx:6-13) and against the
+streaming pass on the same board (GOL_RESIDENT_MAX_CELLS=0 forces the streaming pass; the C ABI reads the
+variable on every gol_step).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gol():
+    import gameoflifewithactors_amd as g
+    from gameoflifewithactors_amd import _lib
+
+    _lib.load()
+    return g
+
+
+def _rand(h, w, seed, p=0.5):
+    return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
+
+
+def _run(gol, b0, boundary, steps, resident):
+    h, w = b0.shape
+    old = os.environ.get("GOL_RESIDENT_MAX_CELLS")
+    os.environ["GOL_RESIDENT_MAX_CELLS"] = str(1 << 20) if resident else "0"
+    try:
+        with gol.Board(w, h, boundary) as b:
+            b.set_cells(b0)
+            for g in steps:
+                b.step(g)
+            assert b.generation == sum(steps)
+            return b.get_cells()
+    finally:
+        if old is None:
+            os.environ.pop("GOL_RESIDENT_MAX_CELLS", None)
+        else:
+            os.environ["GOL_RESIDENT_MAX_CELLS"] = old
+
+
+# (w, h): packed boards (w % 32 == 0) from one word per row to the 2^19-cell capacity, byte boards
+# (ragged widths) from the 3x3 minimum (gol_create) to the 2^16-cell capacity
+SHAPES = [(32, 3), (32, 7), (64, 3), (96, 40), (256, 256), (1024, 512), (512, 1024),
+          (3, 3), (5, 4), (3, 11), (100, 100), (33, 17), (255, 257)]
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", SHAPES)
+def test_resident_matches_oracle_and_streaming(gol, oracle, w, h, boundary):
+    b0 = _rand(h, w, 7 * w + h + boundary)
+    steps = [1, 37, 0, 62]  # several calls: the resident launch ping-pongs the board buffers
+    want = oracle.run(b0, sum(steps), boundary)
+    got = _run(gol, b0, boundary, steps, resident=True)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(_run(gol, b0, boundary, steps, resident=False), want)
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_resident_long_run(gol, oracle, boundary):
+    # 256^2 bounded / torus over 3000 generations in one call (BASELINE config-5 style long run)
+    b0 = _rand(256, 256, 5150 + boundary, p=0.3)
+    np.testing.assert_array_equal(_run(gol, b0, boundary, [3000], resident=True), oracle.run(b0, 3000, boundary))
+
+
+def test_resident_byte_input_values_normalised(gol, oracle):
+    # nonzero = alive on input (set_cells bytes), 0/1 after a step, as on the per-generation byte kernel
+    w, h = 50, 40
+    b0 = _rand(h, w, 99) * np.uint8(255)
+    got = _run(gol, b0, 0, [5], resident=True)
+    np.testing.assert_array_equal(got, oracle.run((b0 != 0).astype(np.uint8), 5, 0))
