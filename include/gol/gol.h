@@ -97,7 +97,9 @@ int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y);
 int gol_clear(gol_board* b);
 
 /* Advance `generations` synchronous B3/S23 generations (GameOfLifeLogic.fs:47-66 under the Reset->State
- * phase barrier).  Asynchronous with respect to the host; any readback synchronises. */
+ * phase barrier).  Asynchronous with respect to the host; any readback synchronises.  Small boards
+ * (packed <= 2^17 cells, bytes <= 2^14; env GOL_RESIDENT_MAX_CELLS overrides) run the whole call as one
+ * LDS-resident launch; results are identical either way. */
 int gol_step(gol_board* b, int64_t generations);
 int gol_generation(gol_board* b, int64_t* out);
 int gol_synchronize(gol_board* b);
