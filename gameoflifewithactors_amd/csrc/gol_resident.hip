@@ -17,10 +17,11 @@
 #include "gol_internal.h"
 #include "gol_bitlogic.h"
 
+#include <cstdlib>
+
 namespace gol {
 namespace {
 
-constexpr int kThreads = 1024;
 constexpr int kLdsBytes = 128 * 1024;
 
 // Work split shared by both kernels: `cols` columns (words or cells) x `nseg` row segments, one
@@ -53,20 +54,20 @@ __device__ __forceinline__ uint32_t packed_row(const uint32_t* a, int wpr, int H
     return m;
 }
 
-template <bool BOUNDED>
-__global__ __launch_bounds__(kThreads) void gol_resident_packed(const uint32_t* __restrict__ src,
+template <bool BOUNDED, int NT>
+__global__ __launch_bounds__(NT) void gol_resident_packed(const uint32_t* __restrict__ src,
                                                                   uint32_t* __restrict__ dst, int wpr, int H,
                                                                   int64_t pitch, int gens, int nseg) {
     __shared__ uint32_t lds[kLdsBytes / 4];
     const int n = wpr * H, items = wpr * nseg;
     uint32_t* a = lds;
     uint32_t* b = lds + n;
-    for (int i = threadIdx.x; i < n; i += kThreads) a[i] = src[(int64_t)(i / wpr) * pitch + i % wpr];
+    for (int i = threadIdx.x; i < n; i += NT) a[i] = src[(int64_t)(i / wpr) * pitch + i % wpr];
     __syncthreads();
     int c0 = 0, y00 = 0, y10 = 0;  // this thread's first item, fixed over the generations
     if ((int)threadIdx.x < items) item_rows(threadIdx.x, wpr, nseg, H, c0, y00, y10);
     for (int g = 0; g < gens; g++) {
-        for (int it = threadIdx.x; it < items; it += kThreads) {
+        for (int it = threadIdx.x; it < items; it += NT) {
             int c = c0, y0 = y00, y1 = y10;
             if (it != (int)threadIdx.x) item_rows(it, wpr, nseg, H, c, y0, y1);
             uint32_t sP, cP, sC, cC, sN, cN;
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void gol_resident_packed(const uint32_t* 
         a = b;
         b = t;
     }
-    for (int i = threadIdx.x; i < n; i += kThreads) dst[(int64_t)(i / wpr) * pitch + i % wpr] = a[i];
+    for (int i = threadIdx.x; i < n; i += NT) dst[(int64_t)(i / wpr) * pitch + i % wpr] = a[i];
 }
 
 // Byte board (nonzero = alive on input, 0/1 on output like gol_bytes_step).
@@ -104,20 +105,20 @@ __device__ __forceinline__ int bytes_row(const uint8_t* a, int W, int H, int x, 
     return l + m + r;
 }
 
-template <bool BOUNDED>
-__global__ __launch_bounds__(kThreads) void gol_resident_bytes(const uint8_t* __restrict__ src,
+template <bool BOUNDED, int NT>
+__global__ __launch_bounds__(NT) void gol_resident_bytes(const uint8_t* __restrict__ src,
                                                                  uint8_t* __restrict__ dst, int W, int H, int gens,
                                                                  int nseg) {
     __shared__ uint8_t lds[kLdsBytes];
     const int n = W * H, items = W * nseg;
     uint8_t* a = lds;
     uint8_t* b = lds + n;
-    for (int i = threadIdx.x; i < n; i += kThreads) a[i] = src[i] != 0;
+    for (int i = threadIdx.x; i < n; i += NT) a[i] = src[i] != 0;
     __syncthreads();
     int x0 = 0, y00 = 0, y10 = 0;  // this thread's first item, fixed over the generations
     if ((int)threadIdx.x < items) item_rows(threadIdx.x, W, nseg, H, x0, y00, y10);
     for (int g = 0; g < gens; g++) {
-        for (int it = threadIdx.x; it < items; it += kThreads) {
+        for (int it = threadIdx.x; it < items; it += NT) {
             int x = x0, y0 = y00, y1 = y10, mP, mC, mN;
             if (it != (int)threadIdx.x) item_rows(it, W, nseg, H, x, y0, y1);
             int hP = bytes_row<BOUNDED>(a, W, H, x, y0 - 1, mP);
@@ -135,13 +136,39 @@ __global__ __launch_bounds__(kThreads) void gol_resident_bytes(const uint8_t* __
         a = b;
         b = t;
     }
-    for (int i = threadIdx.x; i < n; i += kThreads) dst[i] = a[i];
+    for (int i = threadIdx.x; i < n; i += NT) dst[i] = a[i];
 }
 
 // Row segments per column: enough items to give every thread one (at least one row each).
-int segments(int64_t cols, int64_t H) {
-    const int64_t s = cols >= kThreads ? 1 : kThreads / cols;
+int segments(int64_t cols, int64_t H, int nt) {
+    const int64_t s = cols >= nt ? 1 : nt / cols;
     return (int)(s < H ? s : H);
+}
+
+// Workgroup size: 1024 threads unless GOL_RESIDENT_THREADS=256 (A/B of the barrier cost on tiny boards).
+int resident_threads() {
+    const char* e = std::getenv("GOL_RESIDENT_THREADS");
+    return e && std::atoi(e) == 256 ? 256 : 1024;
+}
+
+template <bool BOUNDED>
+void launch_packed(const uint32_t* src, uint32_t* dst, int wpr, int H, int64_t pitch, int gens, hipStream_t s) {
+    if (resident_threads() == 256)
+        hipLaunchKernelGGL((gol_resident_packed<BOUNDED, 256>), dim3(1), dim3(256), 0, s, src, dst, wpr, H, pitch,
+                           gens, segments(wpr, H, 256));
+    else
+        hipLaunchKernelGGL((gol_resident_packed<BOUNDED, 1024>), dim3(1), dim3(1024), 0, s, src, dst, wpr, H, pitch,
+                           gens, segments(wpr, H, 1024));
+}
+
+template <bool BOUNDED>
+void launch_bytes(const uint8_t* src, uint8_t* dst, int W, int H, int gens, hipStream_t s) {
+    if (resident_threads() == 256)
+        hipLaunchKernelGGL((gol_resident_bytes<BOUNDED, 256>), dim3(1), dim3(256), 0, s, src, dst, W, H, gens,
+                           segments(W, H, 256));
+    else
+        hipLaunchKernelGGL((gol_resident_bytes<BOUNDED, 1024>), dim3(1), dim3(1024), 0, s, src, dst, W, H, gens,
+                           segments(W, H, 1024));
 }
 
 }  // namespace
@@ -156,11 +183,9 @@ hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W,
                                   int64_t gens, bool bounded, hipStream_t s) {
     if (!resident_packed_fits(W, H) || pitch < W / 32 || gens < 1 || gens > INT32_MAX) return hipErrorInvalidValue;
     if (bounded)
-        hipLaunchKernelGGL((gol_resident_packed<true>), dim3(1), dim3(kThreads), 0, s, src, dst, (int)(W / 32), (int)H,
-                           pitch, (int)gens, segments(W / 32, H));
+        launch_packed<true>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s);
     else
-        hipLaunchKernelGGL((gol_resident_packed<false>), dim3(1), dim3(kThreads), 0, s, src, dst, (int)(W / 32),
-                           (int)H, pitch, (int)gens, segments(W / 32, H));
+        launch_packed<false>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s);
     return hipGetLastError();
 }
 
@@ -168,11 +193,9 @@ hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, in
                                  hipStream_t s) {
     if (!resident_bytes_fits(W, H) || gens < 1 || gens > INT32_MAX) return hipErrorInvalidValue;
     if (bounded)
-        hipLaunchKernelGGL((gol_resident_bytes<true>), dim3(1), dim3(kThreads), 0, s, src, dst, (int)W, (int)H,
-                           (int)gens, segments(W, H));
+        launch_bytes<true>(src, dst, (int)W, (int)H, (int)gens, s);
     else
-        hipLaunchKernelGGL((gol_resident_bytes<false>), dim3(1), dim3(kThreads), 0, s, src, dst, (int)W, (int)H,
-                           (int)gens, segments(W, H));
+        launch_bytes<false>(src, dst, (int)W, (int)H, (int)gens, s);
     return hipGetLastError();
 }
 
