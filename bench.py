@@ -75,43 +75,113 @@ def parse():
                    help="time the AUTOTUNE depths on the box and keep the faster (agreed across ranks)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU actor baseline sample length")
-    p.add_argument("--cpu-board", type=int, default=512, help="CPU actor baseline board side")
+    p.add_argument("--cpu-seconds", type=float, default=8.0,
+                   help="CPU baseline sample length (C2 actor sample, fair-CPU sample)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="N > 1: nccl (= RCCL over xGMI, the product path) or gloo (host-staged halo; lets "
                    "several ranks share one GPU in rehearsals)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--handle-parts", type=int, default=-1,
+                   help="one-process C-ABI leg (gol_create_multi, csrc/gol_multi.cpp: what the F# drop-in calls): "
+                   "the same board in P row strips on devices 0..P-1 (round-robin over the visible devices, so "
+                   "a one-GPU box rehearses it with every strip on device 0), timed by rank 0 after the main "
+                   "leg; -1 = the world size when N > 1, else off; 0 = off")
     return p.parse_args()
 
 
-def cpu_baseline(args):
-    """The C++ actor-protocol restatement (oracle/actor_protocol.cpp: GameOfLifeLogic.fs:39-71 message for
-    message) on this host's cores, bounded sample (~args.cpu_seconds of wall time)."""
-    exe = os.path.join(ROOT, "oracle", "build", "actor_protocol")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n = args.cpu_board
-    out = subprocess.run([exe, str(n), str(n), "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"],
-                         check=True, capture_output=True, text=True, timeout=600).stdout
-    r = json.loads(out)
+def _cpu_model() -> str:
     cpu = platform.processor() or ""
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return cpu
+
+
+def _run_json(cmd, timeout=900):
+    return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout).stdout)
+
+
+def cpu_baseline(args):
+    """CPU baselines on this host's cores, outside the timed region, rank 0 at N = 1.
+
+    The reference's actors, restated message for message (oracle/actor_protocol.cpp: GameOfLifeLogic.fs:39-71
+    under the Reset->State barrier, 18 messages per cell per generation, the driver of
+    GameOfLifeDriver.fs:13-41), timed at
+      * C1: the reference's own board, 100^2 torus, dotnet-mod2 seeds 0 / 1 / 42, 100 generations each;
+      * C2: 4096^2 torus, dotnet-mod2 seed 42, a bounded sample of whole generations (>= 1; ~14 GB of actor
+        state -- the largest board timed: 65536^2 as actors would need ~3.6 TB).
+    `value` is the C2 figure.  `fair_cpu`: the bit-sliced multithreaded stepper (oracle/gol_fast.c, the
+    carry-save oracle) on the bench workload itself, 65536^2 torus, a bounded sample."""
+    odir = os.path.join(ROOT, "oracle", "build")
+    exe, fast = os.path.join(odir, "actor_protocol"), os.path.join(odir, "gol_fast_bench")
+    if not (os.path.exists(exe) and os.path.exists(fast)):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    cpu = _cpu_model()
+    c1 = {}
+    for seed in (0, 1, 42):
+        r = _run_json([exe, "100", "100", "100", str(threads), str(seed), "0", "dotnet-mod2"])
+        c1[str(seed)] = {"gcups": r["cell_updates_per_s"] / 1e9, "seconds": round(r["seconds"], 3),
+                         "generations": r["generations"], "messages": r["messages"], "hash": str(r["hash"])}
+    c2 = _run_json([exe, "4096", "4096", "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"])
+    fair = _run_json([fast, str(args.width), str(args.width), "0", str(threads), str(args.cpu_seconds)])
     return {
-        "value": r["cell_updates_per_s"] / 1e9,
+        "value": c2["cell_updates_per_s"] / 1e9,
         "unit": "GCUPS",
         "cores": threads,
         "kind": "port",
-        "sample": f"actor-protocol restatement, {n}x{n} torus, dotnet-mod2 seed 42, {r['generations']} generations "
-        f"in {r['seconds']:.1f} s, {r['messages']} messages, {threads} threads on {cpu}",
+        "sample": f"actor-protocol restatement (oracle/actor_protocol.cpp), C2 4096x4096 torus, dotnet-mod2 seed "
+        f"42, {c2['generations']} generation(s) in {c2['seconds']:.1f} s, {c2['messages']} messages, {threads} "
+        f"threads on {cpu}",
+        "c1_100x100_100gens": {
+            "gcups_by_seed": {k: round(v["gcups"], 6) for k, v in c1.items()},
+            "seconds_by_seed": {k: v["seconds"] for k, v in c1.items()},
+            "messages_per_run": c1["42"]["messages"],
+            "board": "100x100 torus (GameOfLifeLogic.fs:5), dotnet-mod2 seeds 0/1/42, 100 generations",
+        },
+        "fair_cpu": {
+            "value": fair["cell_updates_per_s"] / 1e9,
+            "unit": "GCUPS",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"bit-sliced carry-save stepper (oracle/gol_fast.c, AVX-512 build), {fair['width']}x"
+            f"{fair['height']} torus splitmix 0x5EED, {fair['generations']} generations in {fair['seconds']:.1f} s",
+        },
+    }
+
+
+def handle_leg(args, W, H, boundary, parts, ndev):
+    """Time the one-process multi-GPU handle on the bench board: warmup passes, then args.steps passes of
+    its depth, host wall time around gol_step + gol_synchronize; then one pass with per-strip HIP timing
+    events (gol_pass_timing): interior launch, edge-band wait (halo peer copies landed), edge bands."""
+    from gameoflifewithactors_amd import Board
+
+    devices = [i % ndev for i in range(parts)]
+    with Board(W, H, boundary, devices=devices) as b:
+        k = b.parts()[0]["ghost"] if parts > 1 else b.info()["tblock_k"]
+        b.seed_splitmix(args.seed)
+        b.step(args.warmup * k)
+        b.synchronize()
+        t0 = time.perf_counter()
+        b.step(args.steps * k)
+        b.synchronize()
+        dt = time.perf_counter() - t0
+        timing = b.pass_timing()
+    return {
+        "value": round(W * H * args.steps * k / dt / 1e9, 3),
+        "unit": "GCUPS",
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "generations_per_step": k,
+        "strips": parts,
+        "devices": devices,
+        "transport": "hipMemcpyPeerAsync halo rows (xGMI peer copies), one process",
+        "pass_timing_us": timing,
+        "edge_wait_us_max": max(t["edge_wait_us"] for t in timing),
     }
 
 
@@ -137,11 +207,16 @@ def main():
     # one GPU per rank; a gloo rehearsal may place several ranks on one GPU
     dev = local if args.dist_backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    host_group = None
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            # host-side barrier for the handle leg: the waiting ranks must not keep an RCCL kernel spinning
+            # on the devices rank 0's one-process board is running on
+            host_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
+            host_group = dist.group.WORLD
 
     from gameoflifewithactors_amd import TORUS, BOUNDED
     from gameoflifewithactors_amd.strips import StripRunner
@@ -262,11 +337,27 @@ def main():
     tr = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}") or {}
     traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)
 
+    # One-process C-ABI leg (rank 0), after the main leg; the other ranks wait on a host barrier.
+    parts = args.handle_parts if args.handle_parts >= 0 else (world if world > 1 else 0)
+    handle = None
+    if parts >= 1:
+        if world > 1:
+            torch.cuda.synchronize()
+            dist.barrier(group=host_group)
+        if rank == 0:
+            try:
+                handle = handle_leg(args, W, H, boundary, parts, torch.cuda.device_count())
+            except Exception as e:  # reported, never fatal to the main line
+                handle = {"error": f"{type(e).__name__}: {e}"}
+        if world > 1:
+            dist.barrier(group=host_group)
+
     result = None
     if rank == 0:
         result = {
-            "metric": "cell updates/sec (GCUPS) at 65536^2 per GPU",
+            "metric": "cell updates/sec (GCUPS), whole job over all GPUs, 65536^2 cells per GPU; % of HBM peak BW",
             "value": round(gcups, 3),
+            "value_per_gpu": round(gcups / world, 3),
             "unit": "GCUPS",
             "n_gpus": world,
             "steps": args.steps,
@@ -314,6 +405,8 @@ def main():
             "roofline_k1_stream": k1,
             "hbm_copy_measured_gbs": copy_gbs,
         }
+        if handle is not None:
+            result["handle_leg"] = handle
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure (rank 0 only)
             result["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(result), flush=True)

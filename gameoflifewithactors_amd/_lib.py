@@ -91,13 +91,15 @@ SIGNATURES = {
     "gol_hash": (ctypes.c_int, [vp, u64p]),
     "gol_info": (ctypes.c_int, [vp, i64p, i64p, ip, ip, ip]),
     "gol_stream": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    "gol_pass_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "gol_layout": (ctypes.c_int, [vp, ip, i64p]),
     "gol_default_ilv": (ctypes.c_int, [i64]),
     "gol_default_tblock": (ctypes.c_int, [ctypes.c_int]),
     "gol_supported_k": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
-    "gol_fullrow_wg": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int]),
     "gol_last_error": (ctypes.c_char_p, []),
     "gol_version": (ctypes.c_char_p, []),
+    "gol_arch_supported": (ctypes.c_int, [ctypes.c_char_p]),
     "gol_strip_step": (ctypes.c_int, [sp, vp, vp, ctypes.c_int, i64, i64, vp]),
     "gol_strip_seed_splitmix": (ctypes.c_int, [sp, vp, u64, vp]),
     "gol_strip_pack": (ctypes.c_int, [sp, vp, vp, vp]),

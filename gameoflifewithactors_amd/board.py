@@ -198,3 +198,14 @@ class Board:
                   "gol_part_info")
             out.append({"device": d.value, "y0": y0.value, "rows": rows.value, "ghost": ghost.value})
         return out
+
+    def pass_timing(self) -> list:
+        """Advance one pass of the board's temporal depth with HIP timing events (gol_pass_timing); per row
+        strip, microseconds from the pass start to the interior launch's end, to the edge-band stream's
+        release (the halo rows landed: the edge-band wait) and to the edge bands' end."""
+        n = ctypes.c_int()
+        check(self._lib.gol_num_parts(self._h, ctypes.byref(n)), "gol_num_parts")
+        arrs = [(ctypes.c_double * n.value)() for _ in range(3)]
+        check(self._lib.gol_pass_timing(self._h, n.value, *arrs), "gol_pass_timing")
+        return [{"interior_us": round(arrs[0][i], 2), "edge_wait_us": round(arrs[1][i], 2),
+                 "edge_done_us": round(arrs[2][i], 2)} for i in range(n.value)]

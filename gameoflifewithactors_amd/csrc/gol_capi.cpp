@@ -28,7 +28,7 @@ struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
+        if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
     }
     ~DeviceGuard() {
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -165,6 +165,7 @@ constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 // 1.49; byte boards 100^2 2.10 vs 3.56, but 255x257 10.7 vs 3.4.
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
+constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
 
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
@@ -234,10 +235,10 @@ struct gol_board {
 
 namespace {
 
+// The entry points switch to the board's device through DeviceGuard (constructed after this check), which
+// restores the caller's current device on return.
 int check_board(gol_board* b) {
     if (!b) return fail(GOL_ERR_INVALID, "null board");
-    hipError_t e = hipSetDevice(b->device);
-    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
     return GOL_OK;
 }
 
@@ -324,7 +325,9 @@ int step_impl(gol_board* b, int64_t gens) {
         (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
         const bool bounded = b->boundary == GOL_BOUNDED;
         while (gens > 0) {
-            const int64_t g = gens < INT32_MAX ? gens : INT32_MAX;
+            // one launch per 2^16 generations (a few tens of ms): a long gol_step stays interruptible by
+            // readbacks and other work on the board's stream
+            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
             if (b->packed)
                 GOL_HIP(gol::launch_resident_packed(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, g,
                                                     bounded, b->stream));
@@ -409,7 +412,13 @@ extern "C" {
 
 const char* gol_last_error(void) { return g_last_error.c_str(); }
 
-const char* gol_version(void) { return "gol_hip 0.1 (gfx950)"; }
+const char* gol_version(void) { return "gol_hip 0.2 (gfx950)"; }
+
+int gol_arch_supported(const char* gcn_arch_name) {
+    // gcnArchName is "gfx950" or "gfx950:sramecc+:xnack-": the code object is built for gfx950 only
+    if (!gcn_arch_name || std::strncmp(gcn_arch_name, "gfx950", 6) != 0) return 0;
+    return gcn_arch_name[6] == '\0' || gcn_arch_name[6] == ':';
+}
 
 uint64_t gol_hash_finalize(uint64_t h, int64_t width, int64_t height) {
     auto fmix = [](uint64_t k) {
@@ -448,6 +457,20 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         if (devices)
             for (int i = 0; i < n; i++)
                 if (devices[i] < 0 || devices[i] >= ndev) return fail(GOL_ERR_INVALID, "device index out of range");
+        DeviceGuard restore(-1);  // the caller's current device is restored on return
+        {
+            int cur = 0;
+            if (hipGetDevice(&cur) != hipSuccess) return fail(GOL_ERR_NO_DEVICE, "no current HIP device");
+            for (int i = 0; i < (devices ? n : 1); i++) {
+                const int d = devices ? devices[i] : cur;
+                hipDeviceProp_t prop;
+                if (hipGetDeviceProperties(&prop, d) != hipSuccess)
+                    return fail(GOL_ERR_NO_DEVICE, "hipGetDeviceProperties failed");
+                if (!gol_arch_supported(prop.gcnArchName))
+                    return fail(GOL_ERR_NO_DEVICE, std::string("device ") + std::to_string(d) + " is " +
+                                                       prop.gcnArchName + ", this build runs on gfx950 only");
+            }
+        }
         if (n > 1 && width % 32)
             return fail(GOL_ERR_UNSUPPORTED, "a multi-GPU board needs width % 32 == 0 (bit-packed layout)");
         if (n > 1 && height < n) return fail(GOL_ERR_INVALID, "fewer board rows than GPUs");
@@ -569,7 +592,7 @@ int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* row
 
 int gol_destroy(gol_board* b) {
     if (!b) return fail(GOL_ERR_INVALID, "null board");
-    (void)hipSetDevice(b->device);
+    DeviceGuard dg(b->device);
     if (b->multi)
         (void)b->multi->synchronize();
     else
@@ -814,9 +837,38 @@ int gol_default_tblock(int ilv) {
 
 int gol_supported_k(int k, int ilv) { return gol::stream_supported(k, ilv) ? 1 : 0; }
 
-int gol_fullrow_wg(int64_t width, int ilv, int k) {
-    if (width < 32 || width % 32 || (ilv != 1 && ilv != 2 && ilv != 4)) return 0;
-    return gol::stream_fullrow_wg(width / 32, ilv, k);
+int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, double* edge_us) {
+    if (int rc = check_board(b)) return rc;
+    std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
+    const int parts = b->multi ? b->multi->parts() : 1;
+    if (n != parts || !interior_us || !wait_us || !edge_us)
+        return fail(GOL_ERR_INVALID, "n must equal gol_num_parts and the arrays must be non-null");
+    if (b->multi) return b->multi->timed_pass(interior_us, wait_us, edge_us, &b->generation);
+    if (!b->packed) return fail(GOL_ERR_UNSUPPORTED, "pass timing needs a bit-packed board");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    GOL_HIP(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    const int k = b->tblock;
+    if (e == hipSuccess) e = hipEventRecord(e0, b->stream);
+    if (e == hipSuccess) {
+        gol::StreamArgs a = b->stream_args(0, b->H, gol::stream_largest_k(k, k, b->ilv));
+        e = gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, gol::stream_largest_k(k, k, b->ilv),
+                                    b->boundary == GOL_BOUNDED, b->boundary == GOL_TORUS, b->stream);
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, b->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("pass timing: ") + hipGetErrorString(e));
+    b->cur ^= 1;
+    b->generation += gol::stream_largest_k(k, k, b->ilv);
+    interior_us[0] = 1e3 * ms;
+    wait_us[0] = 0;
+    edge_us[0] = 1e3 * ms;
+    return GOL_OK;
 }
 
 int gol_stream(gol_board* b, void** stream) {
@@ -839,9 +891,7 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     if (seg_rows) *seg_rows = a.seg;
     if (waves)
         *waves = a.nstrips * a.nsegs *
-                 (a.wg > 0 ? a.wg
-                           : (a.split > 0 ? gol::stream_wpb(k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4
-                                          : 1));
+                 (a.split > 0 ? gol::stream_wpb(k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
     return GOL_OK;
 }
 

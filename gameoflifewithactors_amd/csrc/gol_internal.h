@@ -19,7 +19,6 @@ struct StreamArgs {
     int64_t nstrips;    // filled by plan_stream
     int64_t nsegs;      // filled by plan_stream
     int32_t ilv;        // words per interleaved block (gol_layout.h): 1, 2 or 4
-    int32_t wg;         // filled by plan_stream: full-row workgroup waves (0 = wave strips)
     int32_t split;      // filled by plan_stream: pair split (older wave's share of a pair segment, 1/65536;
                         // 0 = one segment per wave)
     int32_t spare;      // waves to leave free for concurrent launches (plan_stream)
@@ -30,7 +29,6 @@ bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 int64_t stream_strips(int64_t words, int ilv, int k);
-int stream_fullrow_wg(int64_t words, int ilv, int k);
 int stream_pair_split(int k, int ilv);
 int stream_wpb(int k, int ilv, bool bounded, bool wrap);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)

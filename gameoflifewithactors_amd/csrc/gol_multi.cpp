@@ -269,9 +269,11 @@ int MultiBoard::reduce(bool hash, uint64_t* out) {
 //   compute[i]: wait ev_edge[i]
 // A copy into part j's ghost rows is ordered after j's previous pass has read them: the copying part's
 // previous pass waited for j's copies, which waited for j's pass before that.
-int MultiBoard::pass(int k) {
-    for (Part& p : parts_) {
+int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
+    for (size_t i = 0; i < parts_.size(); i++) {
+        Part& p = parts_[i];
         GOL_MHIP(hipSetDevice(p.device));
+        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].t0, p.compute));
         GOL_MHIP(hipEventRecord(p.ev_start, p.compute));
     }
     const size_t row_bytes = (size_t)W_ / 8;  // pitch == width / 32 words
@@ -292,7 +294,8 @@ int MultiBoard::pass(int k) {
         }
         GOL_MHIP(hipEventRecord(p.ev_copied, p.copy));
     }
-    for (Part& p : parts_) {
+    for (size_t i = 0; i < parts_.size(); i++) {
+        Part& p = parts_[i];
         GOL_MHIP(hipSetDevice(p.device));
         const uint32_t* src = p.buf[cur_];
         uint32_t* dst = p.buf[cur_ ^ 1];
@@ -307,16 +310,53 @@ int MultiBoard::pass(int k) {
             s.spare_waves = (int32_t)std::min<int64_t>(w0 + w1, 1 << 20);
             GOL_MRC(gol_strip_step(&s, src, dst, k, lo, hi, p.compute));
         }
+        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].interior, p.compute));
         GOL_MHIP(hipStreamWaitEvent(p.edge, p.ev_start, 0));
         for (int q : {p.up, p.down})
             if (q >= 0) GOL_MHIP(hipStreamWaitEvent(p.edge, parts_[(size_t)q].ev_copied, 0));
+        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].go, p.edge));
         GOL_MRC(gol_strip_step(&p.s, src, dst, k, 0, lo, p.edge));
         GOL_MRC(gol_strip_step(&p.s, src, dst, k, hi, rows, p.edge));
+        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].edge, p.edge));
         GOL_MHIP(hipEventRecord(p.ev_edge, p.edge));
         GOL_MHIP(hipStreamWaitEvent(p.compute, p.ev_edge, 0));
     }
     cur_ ^= 1;
     return GOL_OK;
+}
+
+int MultiBoard::timed_pass(double* interior_us, double* wait_us, double* edge_us, int64_t* done) {
+    std::vector<PassTimer> t(parts_.size());
+    auto destroy = [&t, this]() {
+        for (size_t i = 0; i < t.size(); i++) {
+            (void)hipSetDevice(parts_[i].device);
+            for (hipEvent_t e : {t[i].t0, t[i].interior, t[i].go, t[i].edge})
+                if (e) (void)hipEventDestroy(e);
+        }
+    };
+    int rc = GOL_OK;
+    for (size_t i = 0; i < t.size() && rc == GOL_OK; i++) {
+        if (hipSetDevice(parts_[i].device) != hipSuccess) rc = api_fail(GOL_ERR_HIP, "hipSetDevice");
+        for (hipEvent_t* e : {&t[i].t0, &t[i].interior, &t[i].go, &t[i].edge})
+            if (rc == GOL_OK && hipEventCreate(e) != hipSuccess) rc = api_fail(GOL_ERR_HIP, "hipEventCreate");
+    }
+    if (rc == GOL_OK) rc = pass(max_k_, &t);
+    if (rc == GOL_OK) rc = synchronize();
+    for (size_t i = 0; i < t.size() && rc == GOL_OK; i++) {
+        float a = 0, b = 0, c = 0;
+        if (hipSetDevice(parts_[i].device) != hipSuccess || hipEventElapsedTime(&a, t[i].t0, t[i].interior) != hipSuccess ||
+            hipEventElapsedTime(&b, t[i].t0, t[i].go) != hipSuccess ||
+            hipEventElapsedTime(&c, t[i].t0, t[i].edge) != hipSuccess) {
+            rc = api_fail(GOL_ERR_HIP, "hipEventElapsedTime");
+            break;
+        }
+        interior_us[i] = 1e3 * a;
+        wait_us[i] = 1e3 * b;
+        edge_us[i] = 1e3 * c;
+    }
+    if (rc == GOL_OK) *done += max_k_;
+    destroy();
+    return rc;
 }
 
 int MultiBoard::step(int64_t generations, int64_t* done) {

@@ -48,6 +48,10 @@ class MultiBoard {
     int step(int64_t generations, int64_t* done);      // *done: generations actually advanced
     int reduce(bool hash, uint64_t* out);
     int synchronize();
+    // one pass of the board's depth with timing events (gol_pass_timing): per part, microseconds from the
+    // pass start to the interior launch's end, to the edge stream's release (halo copies landed) and to the
+    // edge bands' end
+    int timed_pass(double* interior_us, double* wait_us, double* edge_us, int64_t* done);
 
     int parts() const { return (int)parts_.size(); }
     const Part& part(int i) const { return parts_[(size_t)i]; }
@@ -56,7 +60,10 @@ class MultiBoard {
     int max_k() const { return max_k_; }
 
    private:
-    int pass(int k);
+    struct PassTimer {  // timing events of one part, recorded only by timed_pass
+        hipEvent_t t0 = nullptr, interior = nullptr, go = nullptr, edge = nullptr;
+    };
+    int pass(int k, std::vector<PassTimer>* timers = nullptr);
     std::vector<Part> parts_;
     int64_t W_ = 0, H_ = 0;
     int boundary_ = GOL_TORUS, ilv_ = 1, tblock_ = 1, max_k_ = 1;

@@ -8,8 +8,15 @@
 // (one 4*M-byte vector load per lane) is pushed through K generations held in registers -- per
 // generation level a 3-row window of horizontal row sums -- so a pass reads and writes the board once
 // per K generations.  Neighbour words come from the lane's own registers (interleaved layout), the
-// block-edge words from the neighbouring lanes (DPP wave_shr:1 and ds_bpermute), bit carries from
-// v_alignbit_b32, counts from v_bitop3_b32 (gol_bitlogic.h).  No LDS arrays, no barriers, no atomics.
+// block-edge words from the neighbouring lanes (DPP wave_shr:1 / wave_shl:1), bit carries from
+// v_alignbit_b32, counts from v_bitop3_b32 (gol_bitlogic.h).  No LDS, no barriers, no atomics.
+//
+// Variants measured and removed from this file (DESIGN.md 4.1 "Negative results"; the logs stay under
+// profiles/r1/): full-row workgroups with an LDS edge exchange (fullrow_sweep.log), ds_bpermute cross-lane
+// moves in one or both directions (ab_xlane2.log, variant_job_ab.log), batched / late exchanges
+// (ab_early.log), breadth-first levels (ab_breadth.log), per-row-pair fences (ab_fence.log), s_setprio
+// fairness (tail_*.log), 8-row trips (ab_r8.log) and the no-memory / no-arithmetic ceiling builds
+// (ceiling_ab.log).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -24,72 +31,34 @@
 namespace gol {
 
 static constexpr int kWave = 64;
-static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip
+static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip (deep passes)
 // 8 waves per workgroup: the deep passes run 2-3 waves per SIMD, so a workgroup spans the CU's SIMDs
 // twice (profiles/r1/ab_fence2.log: +3-6 % at K = 16 / 32 over 4-wave workgroups)
 #ifndef GOL_WAVES_PER_BLOCK
 #define GOL_WAVES_PER_BLOCK 8
 #endif
 static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
-// Waves per workgroup of a wave-strip kernel: 4 x the waves each SIMD holds at the kernel's register
-// footprint, so ONE workgroup fills a CU and the waves sharing a SIMD (w, w + 4, w + 8, ...) belong to the
-// same workgroup (their age order is then known: see the group split in plan_stream).  GOL_WPB_LIST
-// entries (K, M, waves) override the default; a 12-wave workgroup also asks the compiler for 3 waves/SIMD.
-#ifndef GOL_WPB_LIST
-#define GOL_WPB_LIST(X) X(12, 2, 12)
-#endif
-// GOL_UNIFORM_SEG: group-segment bounds moved to SGPRs (readfirstlane): 0 = never, 1 = ghost-row variant
-// (strip K = 16 96k -> 105k GCUPS, profiles/r1/ab_uniform.log), 2 = every variant (the single board loses
-// 4-8 %: its register allocation changes)
-#ifndef GOL_UNIFORM_SEG
-#define GOL_UNIFORM_SEG 1
-#endif
-// GOL_WPB_GHOST: the list also applies to the ghost-row torus strip variant (multi-GPU ranks)
-#ifndef GOL_WPB_GHOST
-#define GOL_WPB_GHOST 1
-#endif
-// The list applies to the torus variants (single board and ghost-row strips).  The bounded variant carries
-// row/column masks and spills at the 3-waves/SIMD register budget (profiles/r1/strip_bounded_sweep.log:
-// bounded K = 12 41k GCUPS with 12-wave workgroups, 74k with 8).  The ghost-row variant fits once its
-// segment bounds live in SGPRs (GOL_UNIFORM_SEG; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k).
+// Waves per workgroup of a variant: 4 x the waves each SIMD holds at the kernel's register footprint, so
+// ONE workgroup fills a CU and the waves sharing a SIMD (w, w + 4, w + 8) belong to the same workgroup
+// (their age order is then known: see the group split in plan_stream).  (K, M) = (12, 2) runs 12-wave
+// workgroups at 3 waves/SIMD (168 VGPRs; profiles/r1/w12_sweep*.log) in both torus variants.  The bounded
+// variant carries row/column masks and spills at that budget (profiles/r1/strip_bounded_sweep.log: bounded
+// K = 12 41k GCUPS with 12-wave workgroups, 74k with 8), so it keeps 8.
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct Wpb {
-    static constexpr int value = [] {
-        int w = kWavesPerBlock;
-        if (BOUNDED || (!WRAP_ROWS && !GOL_WPB_GHOST)) return w;
-#define GOL_WPB_ENTRY(K_, M_, W_) \
-    if (K == K_ && M == M_) w = W_;
-        GOL_WPB_LIST(GOL_WPB_ENTRY)
-#undef GOL_WPB_ENTRY
-        return w;
-    }();
+    static constexpr int value = (!BOUNDED && K == 12 && M == 2) ? 12 : kWavesPerBlock;
 };
 
-// Cross-lane exchange of the block-edge words.  Measured on gfx950 (tools/ubench/valu_rates.hip,
-// profiles/r1/valu_rates_gfx950.jsonl): a DPP move costs a half-rate VALU issue slot; ds_bpermute_b32
-// runs on the LDS pipe (no VALU slot, but ~60+ cycles of latency that the waves end up waiting on).
-// GOL_XLANE: 0 = DPP both directions, 1 = ds_bpermute both directions, 2 = left via DPP, right via
-// ds_bpermute.  With the level-fenced schedule, 0 is fastest at every depth (profiles/r1/ab_xlane2.log:
-// +2-5 % over 2, 1 is 6-17 % slower).
-#ifndef GOL_XLANE
-#define GOL_XLANE 0
-#endif
-// GOL_BATCH_XLANE: issue a level's ds_bpermute exchanges for all rows of a trip before its arithmetic
-#ifndef GOL_BATCH_XLANE
-#define GOL_BATCH_XLANE 1
-#endif
-// GOL_EARLY_XLANE: 1 = issue level g+1's right-hand exchange (ds_bpermute) as soon as level g has produced
-// the row, pinned there by a scheduling barrier that only DS instructions may not cross; 2 = the same plus
-// a full scheduling barrier between levels.  Without the level barrier the scheduler interleaves levels
-// and the live register set grows past the occupancy steps (K=16, M=2: 256 VGPRs, 1 wave/SIMD; with it
-// 213 VGPRs, 2 waves/SIMD): profiles/r1/ab_early.log, ab_fence2.log.
-#ifndef GOL_EARLY_XLANE
-#define GOL_EARLY_XLANE 2
-#endif
-// GOL_K1_NOHALO: K = 1 passes use halo-free 64-block strips (StreamWave::kNoHalo)
-#ifndef GOL_K1_NOHALO
-#define GOL_K1_NOHALO 1
-#endif
+// Block-edge words of the neighbouring lanes, by DPP (a half-rate VALU move on gfx950,
+// profiles/r1/valu_rates_gfx950.jsonl).  ds_bpermute_b32 in either direction measured 2-17 % slower under
+// the level-fenced schedule below (its ~60-cycle latency; profiles/r1/ab_xlane2.log).
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i-1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);  // wave_shr:1
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
+}
+
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
 // into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
 #ifndef GOL_STAMP
@@ -100,33 +69,7 @@ static constexpr int kStamps = 1 << 16;
 __device__ unsigned long long g_stamps[2][kStamps];
 #endif
 // sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
-[[maybe_unused]] static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
-// Measured and removed: breadth-first levels (profiles/r1/ab_breadth.log), per-row-pair
-// fences (ab_fence.log), s_setprio fairness between SIMD partners (tail_*.log), 8-row trips (ab_r8.log).
-// GOL_DEBUG_MODE (ceiling experiments only, results are wrong): 1 = no memory traffic (synthetic rows,
-// outputs folded into one register), 2 = no arithmetic (the pass copies the board)
-#ifndef GOL_DEBUG_MODE
-#define GOL_DEBUG_MODE 0
-#endif
-struct XLane {
-    int left_addr, right_addr;  // byte addresses of lane-1 / lane+1 for ds_bpermute
-    __device__ __forceinline__ explicit XLane(int lane)
-        : left_addr(((lane - 1) & 63) << 2), right_addr(((lane + 1) & 63) << 2) {}
-    __device__ __forceinline__ uint32_t from_left(uint32_t v) const {  // lane i <- lane i-1
-#if GOL_XLANE == 1
-        return (uint32_t)__builtin_amdgcn_ds_bpermute(left_addr, (int)v);
-#else
-        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);  // wave_shr:1
-#endif
-    }
-    __device__ __forceinline__ uint32_t from_right(uint32_t v) const {  // lane i <- lane i+1
-#if GOL_XLANE == 0
-        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
-#else
-        return (uint32_t)__builtin_amdgcn_ds_bpermute(right_addr, (int)v);
-#endif
-    }
-};
+static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
 
 // A wave-uniform 64-bit value the compiler cannot prove uniform (e.g. derived from float math), moved to SGPRs
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
@@ -201,40 +144,23 @@ struct TripRows {
     static constexpr int value = (K == 1 && M == 1) ? 8 : 4;  // 8-row deep trips: -2.5 % (ab_r8.log)
 };
 
-// Full-row workgroup mode (WG > 0): the WG * 64 lanes of one workgroup hold one whole board row (one block
-// each, nblocks == 64 * WG), so there are no halo lanes and no partial strips; the block-edge words cross
-// lanes AND waves through an LDS exchange buffer.  Per trip the rows are split into two halves; a half's
-// edge words for level g+1 are published (ds_write_b64), the workgroup meets at a barrier, and their
-// neighbours are read (ds_read) before the OTHER half's level-g arithmetic, which hides the LDS latency:
-// two barriers per level, every wave in lockstep over the same segment.
-// Exchange slot layout: [half][level parity][row in half][1 + lane], with zero pads at index 0 and N + 1
-// (the dead cells beyond a bounded board's left / right edge).
-template <int WG, int R>
-struct WgX {
-    static constexpr int N = 64 * WG;
-    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-    u32x2_t (*x)[2][R / 2][N + 2];
-};
-
 // One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG = 0>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct StreamWave {
     static constexpr int R = TripRows<K, M>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
     using V = Vec<M>;
-    using X = WgX<(WG > 0 ? WG : 1), R>;
-    static constexpr int NL = 64 * (WG > 0 ? WG : 1);  // lanes of a full-row workgroup
     // K = 1 wave strips have no halo lanes: all 64 lanes are stored, and the two words beyond the
     // strip's ends (left of lane 0, right of lane 63) are loaded from memory with the row (one extra
     // dword load per row; lanes 1-62 reload their own word, an L1 hit).  Stores are then whole
-    // 64-block runs: 256 / 512 / 1024 B aligned, instead of 62-block runs at 248 B offsets.
-    static constexpr bool kNoHalo = (K == 1 && WG == 0 && GOL_K1_NOHALO);
+    // 64-block runs: 256 / 512 / 1024 B aligned, instead of 62-block runs at 248 B offsets
+    // (profiles/r1/k1_nohalo_ab.log: 3.9-4.1 -> 4.7-5.1 TB/s).
+    static constexpr bool kNoHalo = K == 1;
     static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
 
     const uint32_t* __restrict__ src;
     uint32_t* __restrict__ dst;
     const StreamArgs& a;
-    XLane xl;
     int load_off;      // this lane's byte offset in a row (its block column)
     int store_off;     // = load_off for interior on-board lanes, kNoStore otherwise
     uint32_t colmask;  // bounded: ~0 for an on-board block
@@ -248,10 +174,6 @@ struct StreamWave {
     // K = 1 halo-free strips: byte offset of this lane's neighbour word, and its bounded-board mask
     int nb_off = 0;
     uint32_t nbmask = 0xffffffffu;
-
-    // full-row workgroup mode: exchange buffer and this lane's slot indices (own, left and right neighbour)
-    X xc;
-    int xme = 0, xleft = 0, xright = 0;
 
     // First row (relative to the group segment of `len` rows) of the i-th oldest wave's share.  Shares
     // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
@@ -273,56 +195,41 @@ struct StreamWave {
         return cut < 0 ? 0 : (cut > len ? len : cut);
     }
 
-    // `lane`: lane within the wave's strip (wave mode) or within the workgroup (full-row mode, sx = 0).
-    // `role`: -1 = the wave owns segment sy; 0 / 1 = the older / younger wave of a SIMD pair sharing
-    // pair-segment sy (split by a.split, see plan_stream)
+    // `lane`: lane within the wave's strip.  `role`: -1 = the wave owns segment sy; 0, 1, ... = the
+    // oldest, next, ... wave of the SIMD group sharing group segment sy (split by a.split, see plan_stream)
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
                                           int64_t sx, int64_t sy, int role = -1)
-        : src(s), dst(d), a(args), xl(lane & 63) {
+        : src(s), dst(d), a(args) {
         const int64_t nblocks = a.words / M;
-        if (WG > 0) {  // block == lane, every lane on the board and stored
-            colmask = 0xffffffffu;
-            load_off = lane * 4 * M;
-            store_off = load_off;
-            xme = lane + 1;
-            if (BOUNDED) {  // beyond the row's ends: the zero pads
-                xleft = lane;
-                xright = lane + 2;
-            } else {  // torus: wrap within the row
-                xleft = lane == 0 ? NL : lane;
-                xright = lane == NL - 1 ? 1 : lane + 2;
-            }
+        // this lane's block column (may be off-board)
+        const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
+        int64_t lc;
+        if (BOUNDED) {
+            const bool in = cb >= 0 && cb < nblocks;
+            colmask = in ? 0xffffffffu : 0u;
+            lc = in ? cb : 0;
         } else {
-            // this lane's block column (may be off-board)
-            const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
-            int64_t lc;
+            colmask = 0xffffffffu;
+            lc = floor_mod(cb, nblocks);
+        }
+        load_off = (int)(lc * 4 * M);
+        if (kNoHalo) {
+            store_off = cb < nblocks ? load_off : kNoStore;
+            // lane 0: last word of the block to the left; lane 63: first word of the block to the right
+            const int64_t nbc = lane == 0 ? cb - 1 : (lane == kWave - 1 ? cb + 1 : lc);
+            const int nbw = lane == 0 ? M - 1 : 0;
+            int64_t nl;
             if (BOUNDED) {
-                const bool in = cb >= 0 && cb < nblocks;
-                colmask = in ? 0xffffffffu : 0u;
-                lc = in ? cb : 0;
+                const bool in = nbc >= 0 && nbc < nblocks;
+                nbmask = in ? 0xffffffffu : 0u;
+                nl = in ? nbc : 0;
             } else {
-                colmask = 0xffffffffu;
-                lc = floor_mod(cb, nblocks);
+                nbmask = 0xffffffffu;
+                nl = floor_mod(nbc, nblocks);
             }
-            load_off = (int)(lc * 4 * M);
-            if (kNoHalo) {
-                store_off = cb < nblocks ? load_off : kNoStore;
-                // lane 0: last word of the block to the left; lane 63: first word of the block to the right
-                const int64_t nbc = lane == 0 ? cb - 1 : (lane == kWave - 1 ? cb + 1 : lc);
-                const int nbw = lane == 0 ? M - 1 : 0;
-                int64_t nl;
-                if (BOUNDED) {
-                    const bool in = nbc >= 0 && nbc < nblocks;
-                    nbmask = in ? 0xffffffffu : 0u;
-                    nl = in ? nbc : 0;
-                } else {
-                    nbmask = 0xffffffffu;
-                    nl = floor_mod(nbc, nblocks);
-                }
-                nb_off = (int)((nl * M + nbw) * 4);
-            } else {
-                store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
-            }
+            nb_off = (int)((nl * M + nbw) * 4);
+        } else {
+            store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
         }
         row_bytes = a.words * 4;
         seg_begin = a.out_begin + sy * a.seg;
@@ -332,10 +239,11 @@ struct StreamWave {
             const int64_t b0 = seg_begin;
             seg_begin = b0 + group_cut(len, role);
             seg_end = b0 + group_cut(len, role + 1);
-            if (GOL_UNIFORM_SEG == 2 || (GOL_UNIFORM_SEG == 1 && !WRAP_ROWS && !BOUNDED)) {
+            if (!WRAP_ROWS && !BOUNDED) {
                 // the group cut is float VALU math: without this the segment bounds live in 8 VGPRs, and
                 // the ghost-row variant spills at the 3-waves/SIMD budget (a scratch reload every loop
-                // trip).  The single-board variant keeps its measured instruction stream.
+                // trip; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k GCUPS).  The single-board
+                // variant loses 4-8 % with it (its register allocation changes), so it keeps VGPR bounds.
                 seg_begin = uniform64(seg_begin);
                 seg_end = uniform64(seg_end);
             }
@@ -364,14 +272,8 @@ struct StreamWave {
                 // step) are never used unmasked: clamp the address into the buffer
                 br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
-#if GOL_DEBUG_MODE == 1
-#pragma unroll
-            for (int j = 0; j < M; j++)
-                buf[r][j] = ((uint32_t)load_off * 0x9E3779B9u) ^ ((uint32_t)br * 0x85EBCA6Bu + (uint32_t)j);
-#else
             V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
             if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
-#endif
             if (BOUNDED) {
                 const int64_t gy = a.y0 + ly0 + first_step + r;
                 const bool row_in = gy >= 0 && gy < a.height;
@@ -402,77 +304,10 @@ struct StreamWave {
 
     // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
-    // ---- full-row workgroup mode
-    // publish rows of half h (their block-edge words are level g's inputs), barrier, read the neighbours
-    __device__ __forceinline__ void wg_publish(const uint32_t (&v)[R][M], int g, int h, uint32_t (&L)[R],
-                                               uint32_t (&Rt)[R]) {
-#pragma unroll
-        for (int i = 0; i < R / 2; i++) {
-            const int r = h * (R / 2) + i;
-            typename X::u32x2_t e = {v[r][0], v[r][M - 1]};
-            xc.x[h][g & 1][i][xme] = e;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#pragma unroll
-        for (int i = 0; i < R / 2; i++) {
-            const int r = h * (R / 2) + i;
-            L[r] = xc.x[h][g & 1][i][xleft].y;   // left neighbour's last word
-            Rt[r] = xc.x[h][g & 1][i][xright].x;  // right neighbour's first word
-        }
-    }
-
-    // level g over the two rows of half h (the same arithmetic as the wave-mode pair below)
-    __device__ __forceinline__ void wg_half(uint32_t (&v)[R][M], int g, int h, int64_t lyt, const uint32_t (&L)[R],
-                                            const uint32_t (&Rt)[R]) {
-#pragma unroll
-        for (int r = h * (R / 2); r < (h + 1) * (R / 2); r += 2) {
-            uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
-            if (BOUNDED) {
-                const int64_t gy = a.y0 + lyt + r - g - 1;
-                m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
-                m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
-            }
-            uint32_t o0[M], o1[M];
-            level_row(v[r], L[r], Rt[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-            level_row(v[r + 1], L[r + 1], Rt[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1, o1);
-#pragma unroll
-            for (int j = 0; j < M; j++) {
-                aY[g][j] = v[r + 1][j];
-                v[r][j] = o0[j];
-                v[r + 1][j] = o1[j];
-            }
-        }
-    }
-
-    template <bool SKIP>
-    __device__ __forceinline__ void process_wg(uint32_t (&v)[R][M], int64_t t) {
-        const int64_t lyt = ly0 + t * R;
-        uint32_t L[R], Rt[R];
-        wg_publish(v, 0, 0, L, Rt);
-        wg_publish(v, 0, 1, L, Rt);
-#pragma unroll
-        for (int g = 0; g < K; g++) {
-            if (SKIP && t * R + R - 1 < 2 * g) break;  // this and every deeper level is pipeline fill
-            const bool next = g + 1 < K && !(SKIP && t * R + R - 1 < 2 * (g + 1));
-            wg_half(v, g, 0, lyt, L, Rt);
-            if (next) wg_publish(v, g + 1, 0, L, Rt);  // its reads overlap the other half's arithmetic
-            wg_half(v, g, 1, lyt, L, Rt);
-            if (next) wg_publish(v, g + 1, 1, L, Rt);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-
     template <bool SKIP>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
-        if (GOL_DEBUG_MODE == 2) return;
-        if constexpr (WG > 0) {
-            process_wg<SKIP>(v, t);
-            return;
-        }
+        const int64_t lyt = ly0 + t * R;
         if constexpr (kNoHalo) {  // K = 1: lanes 0 / 63 keep the loaded neighbour word (bound_ctrl off)
-            const int64_t lyt = ly0 + t * R;
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
@@ -499,25 +334,16 @@ struct StreamWave {
             }
             return;
         }
-        const int64_t lyt = ly0 + t * R;
-#if GOL_EARLY_XLANE
+        // Level g+1's right-hand exchange is issued as soon as level g has produced the row, and a full
+        // scheduling barrier separates the levels: without it the scheduler interleaves levels and the
+        // live register set grows past the occupancy steps (K = 16, M = 2: 256 VGPRs, 1 wave/SIMD; with
+        // it 213, 2 waves/SIMD; profiles/r1/ab_early.log, ab_fence2.log).
         uint32_t right[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) right[r] = xl.from_right(v[r][0]);
-#endif
+        for (int r = 0; r < R; r++) right[r] = from_right(v[r][0]);
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
-#if !GOL_EARLY_XLANE
-            // block-edge words of the right-hand lanes for all R rows first: the LDS-pipe exchanges
-            // (ds_bpermute) then overlap each other and the arithmetic below instead of each stalling
-            // its own row; the DPP (VALU) moves from the left stay next to their use
-            uint32_t right[R];
-#if GOL_BATCH_XLANE
-#pragma unroll
-            for (int r = 0; r < R; r++) right[r] = xl.from_right(v[r][0]);
-#endif
-#endif
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
@@ -528,12 +354,8 @@ struct StreamWave {
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-#if !GOL_BATCH_XLANE && !GOL_EARLY_XLANE
-                right[r] = xl.from_right(v[r][0]);
-                right[r + 1] = xl.from_right(v[r + 1][0]);
-#endif
-                level_row(v[r], xl.from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-                level_row(v[r + 1], xl.from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
+                level_row(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
                           o1);
 #pragma unroll
                 for (int j = 0; j < M; j++) {
@@ -541,27 +363,17 @@ struct StreamWave {
                     v[r][j] = o0[j];
                     v[r + 1][j] = o1[j];
                 }
-#if GOL_EARLY_XLANE
                 if (g + 1 < K) {
-                    right[r] = xl.from_right(o0[0]);
-                    right[r + 1] = xl.from_right(o1[0]);
+                    right[r] = from_right(o0[0]);
+                    right[r + 1] = from_right(o1[0]);
                     __builtin_amdgcn_sched_barrier(kAllButDs);
                 }
-#endif
             }
-#if GOL_EARLY_XLANE == 2
             __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges
-#endif
         }
     }
 
-    uint32_t dbg_acc = 0;
     __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
-#if GOL_DEBUG_MODE == 1
-#pragma unroll
-        for (int j = 0; j < M; j++) dbg_acc ^= v[j];
-        return;
-#endif
         V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? row_bytes : 0), store_off, v);
     }
     // Store trip t's outputs.  Rows outside the segment (pipeline fill and the tail) get an empty
@@ -577,69 +389,46 @@ struct StreamWave {
     }
 };
 
-// Trips: [0, t_fill) pipeline fill (nothing valid to store, garbage levels skipped), then the steady
-// loop.  Loads for trip t+1 are issued before trip t computes (one trip of prefetch); trip t's outputs
-// are stored at the top of trip t+1 (below).
-// Minimum waves per SIMD the register allocator must fit (0 = compiler's choice), per depth and layout.
+// Minimum waves per SIMD the register allocator must fit (1 = compiler's choice), per variant.
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct MinWaves {
     static constexpr int value = Wpb<K, M, BOUNDED, WRAP_ROWS>::value > 8 ? Wpb<K, M, BOUNDED, WRAP_ROWS>::value / 4 : 1;
 };
 
-// WG = 0: wave strips (kWavesPerBlock waves per workgroup, each its own column strip and segment).
-// WG > 0: full-row workgroups of WG waves (one segment per workgroup; requires words / M == 64 * WG).
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int WG>
-__global__ __launch_bounds__(kWave*(WG > 0 ? WG : Wpb<K, M, BOUNDED, WRAP_ROWS>::value))
+// Wave strips: Wpb waves per workgroup, each its own column strip and segment (or a share of a group
+// segment, see plan_stream).
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+__global__ __launch_bounds__((kWave * Wpb<K, M, BOUNDED, WRAP_ROWS>::value))
 __attribute__((amdgpu_waves_per_eu(MinWaves<K, M, BOUNDED, WRAP_ROWS>::value)))
 void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
-    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS, WG>;
+    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS>;
     constexpr int R = W::R;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t sx, sy;
-    int strip_lane, role = -1;
-    if constexpr (WG > 0) {
-        if ((int64_t)blockIdx.x >= a.nsegs) return;  // uniform over the workgroup
-        sx = 0;
-        sy = blockIdx.x;
-        strip_lane = threadIdx.x;
+    int role = -1;
+    // wave index made provably uniform so all row bookkeeping lives in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS>::value;
+    if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
+        const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
+        role = wave >> 2;  // 0 = the oldest
+        if (group >= a.nstrips * a.nsegs) return;
+        sx = group % a.nstrips;
+        sy = group / a.nstrips;
     } else {
-        // wave index made provably uniform so all row bookkeeping lives in SGPRs
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS>::value;
-        if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
-            const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
-            role = wave >> 2;  // 0 = the oldest
-            if (group >= a.nstrips * a.nsegs) return;
-            sx = group % a.nstrips;
-            sy = group / a.nstrips;
-        } else {
-            const int64_t gw = (int64_t)blockIdx.x * WPB + wave;
-            if (gw >= a.nstrips * a.nsegs) return;
-            sx = gw % a.nstrips;
-            sy = gw / a.nstrips;
-        }
-        strip_lane = lane;
+        const int64_t gw = (int64_t)blockIdx.x * WPB + wave;
+        if (gw >= a.nstrips * a.nsegs) return;
+        sx = gw % a.nstrips;
+        sy = gw / a.nstrips;
     }
-    W w(src, dst, a, strip_lane, sx, sy, role);
+    W w(src, dst, a, lane, sx, sy, role);
 #if GOL_STAMP
     const int64_t stamp_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t stamp_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if constexpr (WG > 0) {
-        __shared__ typename W::X::u32x2_t xbuf[2][2][R / 2][64 * WG + 2];
-        constexpr int npad = 2 * 2 * (R / 2);
-        if ((int)threadIdx.x < 2 * npad) {  // zero pads: the dead cells beyond a bounded row's ends
-            const int q = threadIdx.x >> 1;
-            const typename W::X::u32x2_t z = {0u, 0u};
-            xbuf[q / R][(q / (R / 2)) & 1][q % (R / 2)][(threadIdx.x & 1) ? 64 * WG + 1 : 0] = z;
-        }
-        w.xc.x = xbuf;
-        __syncthreads();
-    }
 
     const int64_t ntrips = (w.nsteps + R - 1) / R;
     const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
-    const int64_t first_store_trip = (2 * K + R - 1) / R;
 
     // Trip t (rows of trip t in `cur`, trip t-1's outputs in `other`):
     //   [wait for all memory ops of trip t-1] [store `other`] [prefetch trip t+1 into `other`]
@@ -684,10 +473,6 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(B, t - 1);
     }
-    (void)first_store_trip;
-#if GOL_DEBUG_MODE == 1
-    if (w.dbg_acc == 0x5EED1234u) dst[lane] = w.dbg_acc;
-#endif
 #if GOL_STAMP
     __builtin_amdgcn_s_waitcnt(0);
     if (lane == 0 && stamp_id < kStamps) {
@@ -704,13 +489,6 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     X(1, 1) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(24, 1) X(32, 1)                                           \
     X(1, 2) X(2, 2) X(4, 2) X(8, 2) X(12, 2) X(16, 2)                                                    \
     X(1, 4) X(2, 4) X(4, 4) X(6, 4) X(8, 4)
-
-// Full-row workgroup instantiations (K, M, WG): the row is exactly 64 * WG blocks of M words
-// (65536 cells for (M = 4, WG = 8) and (M = 2, WG = 16)).  WG waves must fit one CU at the kernel's
-// occupancy: 8 waves need <= 256 VGPRs (2 waves/SIMD), 16 need <= 128.  Opt-in (GOL_FULLROW=1): bit-exact,
-// but the two workgroup barriers per level cost more than the halo lanes they remove (65536^2:
-// (4, 8) 81-84k vs 89-91k GCUPS in wave strips, (2, 8) 70k vs 84-89k; profiles/r1/fullrow_sweep.log).
-#define GOL_FOR_EACH_KMW(X) X(4, 4, 8) X(8, 4, 8) X(8, 2, 16)
 
 bool stream_supported(int k, int ilv) {
 #define GOL_SUP(K_, M_) \
@@ -731,48 +509,26 @@ int stream_largest_k(int64_t n, int cap, int ilv) {
 
 // Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
 // (never wraps: rows beyond the board are masked dead).
-template <int K, int M, int WG>
+template <int K, int M>
 static const void* stream_kernel(bool bounded, bool wrap) {
-    if (bounded) return (const void*)&gol_stream_step<K, M, true, false, WG>;
-    return wrap ? (const void*)&gol_stream_step<K, M, false, true, WG>
-                : (const void*)&gol_stream_step<K, M, false, false, WG>;
+    if (bounded) return (const void*)&gol_stream_step<K, M, true, false>;
+    return wrap ? (const void*)&gol_stream_step<K, M, false, true> : (const void*)&gol_stream_step<K, M, false, false>;
 }
 
-static const void* kernel_for(int k, int ilv, int wg, bool bounded, bool wrap) {
-    if (wg == 0) {
+static const void* kernel_for(int k, int ilv, bool bounded, bool wrap) {
 #define GOL_KPTR(K_, M_) \
-    if (k == K_ && ilv == M_) return stream_kernel<K_, M_, 0>(bounded, wrap);
-        GOL_FOR_EACH_KM(GOL_KPTR)
+    if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap);
+    GOL_FOR_EACH_KM(GOL_KPTR)
 #undef GOL_KPTR
-    }
-#define GOL_KWPTR(K_, M_, W_) \
-    if (k == K_ && ilv == M_ && wg == W_) return stream_kernel<K_, M_, W_>(bounded, wrap);
-    GOL_FOR_EACH_KMW(GOL_KWPTR)
-#undef GOL_KWPTR
     return nullptr;
 }
 
-// Full-row workgroup size for a row of `words` words in layout `ilv` at depth k, or 0 (wave strips).
-// GOL_FULLROW=1 enables the mode (experimental until measured).
-int stream_fullrow_wg(int64_t words, int ilv, int k) {
-    static const bool enabled = [] {
-        const char* e = std::getenv("GOL_FULLROW");
-        return e && e[0] == '1';
-    }();
-    if (!enabled || words % ilv) return 0;
-#define GOL_FR(K_, M_, W_) \
-    if (k == K_ && ilv == M_ && words / M_ == 64 * W_) return W_;
-    GOL_FOR_EACH_KMW(GOL_FR)
-#undef GOL_FR
-    return 0;
-}
-
 int64_t stream_strips(int64_t words, int ilv, int k) {
-    const int per = (k == 1 && GOL_K1_NOHALO) ? kWave : kInterior;  // K = 1: halo-free strips
+    const int per = k == 1 ? kWave : kInterior;  // K = 1: halo-free strips
     return (words / ilv + per - 1) / per;
 }
 
-// Waves per workgroup of the wave-strip kernel variant (Wpb)
+// Waves per workgroup of a variant (Wpb)
 int stream_wpb(int k, int ilv, bool bounded, bool wrap) {
     if (bounded) return kWavesPerBlock;
 #define GOL_WPBQ(K_, M_) \
@@ -804,19 +560,18 @@ int stream_pair_split(int k, int ilv) {
     return 0;
 }
 
-// Scheduling units of a stream-kernel variant the current device holds at once (occupancy x CUs):
-// waves in wave mode, workgroups in full-row mode; cached.  Falls back to 4096 waves (or 256
-// workgroups) when no device answers (host-only planning, e.g. CPU tests).
-static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
-    static std::atomic<int64_t> cache[33][5][17][2][2];
-    const int64_t fallback = wg ? 256 : 4096;
-    if (k < 0 || k > 32 || ilv < 1 || ilv > 4 || wg < 0 || wg > 16) return fallback;
+// Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.  Falls back
+// to 4096 waves when no device answers (host-only planning, e.g. CPU tests).
+static int64_t resident_units(int k, int ilv, bool bounded, bool wrap) {
+    static std::atomic<int64_t> cache[33][5][2][2];
+    const int64_t fallback = 4096;
+    if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return fallback;
     if (bounded) wrap = false;
-    int64_t v = cache[k][ilv][wg][bounded][wrap].load(std::memory_order_relaxed);
+    int64_t v = cache[k][ilv][bounded][wrap].load(std::memory_order_relaxed);
     if (v > 0) return v;
-    const void* fn = kernel_for(k, ilv, wg, bounded, wrap);
+    const void* fn = kernel_for(k, ilv, bounded, wrap);
     const int wpb = stream_wpb(k, ilv, bounded, wrap);
-    const int threads = kWave * (wg ? wg : wpb);
+    const int threads = kWave * wpb;
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -825,23 +580,22 @@ static int64_t resident_units(int k, int ilv, int wg, bool bounded, bool wrap) {
         (void)hipGetLastError();
         return fallback;
     }
-    v = (int64_t)blocks * cus * (wg ? 1 : wpb);
-    cache[k][ilv][wg][bounded][wrap].store(v, std::memory_order_relaxed);
+    v = (int64_t)blocks * cus * wpb;
+    cache[k][ilv][bounded][wrap].store(v, std::memory_order_relaxed);
     return v;
 }
 
-// Work decomposition: nstrips column strips x nsegs row segments, one wave each (full-row mode: one
-// strip, one workgroup per segment).  The segment count makes the grid ONE balanced round of resident
-// units (a partial second round would leave a tail of lone waves), with segments no shorter than 2K
-// rows (pipeline fill cost).  GOL_SEG_ROWS overrides the segment length (experiments).
+// Work decomposition: nstrips column strips x nsegs row segments, one wave each (or one SIMD group of
+// waves per segment with the pair split).  The segment count makes the grid ONE balanced round of
+// resident waves (a partial second round would leave a tail of lone waves), with segments no shorter than
+// 2K rows (pipeline fill cost).  GOL_SEG_ROWS overrides the segment length (experiments).
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     static const int64_t env_seg = [] {
         const char* e = std::getenv("GOL_SEG_ROWS");
         return e ? std::atoll(e) : 0LL;
     }();
-    a.wg = stream_fullrow_wg(a.words, a.ilv, k);
-    a.split = a.wg ? 0 : stream_pair_split(k, a.ilv);
-    a.nstrips = a.wg ? 1 : stream_strips(a.words, a.ilv, k);
+    a.split = stream_pair_split(k, a.ilv);
+    a.nstrips = stream_strips(a.words, a.ilv, k);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
         a.nsegs = 0;
@@ -855,8 +609,8 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     int64_t seg = env_seg;
     if (seg <= 0) {
         const int group = a.split ? wpb / 4 : 1;  // waves per segment
-        int64_t units = resident_units(k, a.ilv, a.wg, bounded, wrap);
-        if (!a.wg && a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
+        int64_t units = resident_units(k, a.ilv, bounded, wrap);
+        if (a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
         const int64_t slots = units / group;
         int64_t nsegs = slots / a.nstrips;
         if (nsegs < 1) nsegs = 1;
@@ -874,27 +628,20 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     a.nsegs = (rows + seg - 1) / seg;
 }
 
-template <int K, int M, int WG>
-static hipError_t launch_kmw(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
-                             hipStream_t s) {
-    unsigned blocks;
-    dim3 block;
-    if (WG > 0) {
-        blocks = (unsigned)a.nsegs;
-        block = dim3(kWave * WG);
-    } else {
-        const int WPB = stream_wpb(K, M, bounded, wrap);
-        const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
-        blocks = (unsigned)((waves + WPB - 1) / WPB);
-        block = dim3(kWave * WPB);
-    }
+template <int K, int M>
+static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
+                            hipStream_t s) {
+    const int WPB = stream_wpb(K, M, bounded, wrap);
+    const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
+    const unsigned blocks = (unsigned)((waves + WPB - 1) / WPB);
+    const dim3 block(kWave * WPB);
     if (bounded) {
-        hipLaunchKernelGGL((gol_stream_step<K, M, true, false, WG>), dim3(blocks), block, 0, s, src, dst, a);
+        hipLaunchKernelGGL((gol_stream_step<K, M, true, false>), dim3(blocks), block, 0, s, src, dst, a);
     } else {
         if (wrap)
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, true, WG>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, true>), dim3(blocks), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, false, WG>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, false>), dim3(blocks), block, 0, s, src, dst, a);
     }
     return hipGetLastError();
 }
@@ -903,15 +650,8 @@ hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, 
                               hipStream_t s) {
     plan_stream(a, k, bounded, wrap);
     if (a.nsegs <= 0) return hipSuccess;
-    if (a.wg > 0) {
-#define GOL_LAUNCH_W(K_, M_, W_) \
-    if (k == K_ && a.ilv == M_ && a.wg == W_) return launch_kmw<K_, M_, W_>(src, dst, a, bounded, wrap, s);
-        GOL_FOR_EACH_KMW(GOL_LAUNCH_W)
-#undef GOL_LAUNCH_W
-        return hipErrorInvalidValue;
-    }
 #define GOL_LAUNCH(K_, M_) \
-    if (k == K_ && a.ilv == M_) return launch_kmw<K_, M_, 0>(src, dst, a, bounded, wrap, s);
+    if (k == K_ && a.ilv == M_) return launch_km<K_, M_>(src, dst, a, bounded, wrap, s);
     GOL_FOR_EACH_KM(GOL_LAUNCH)
 #undef GOL_LAUNCH
     return hipErrorInvalidValue;

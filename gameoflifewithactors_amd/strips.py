@@ -372,13 +372,19 @@ class LocalBoard:
         for r in self.runners:
             r.seed_splitmix(seed)
 
-    def hash(self) -> int:
+    def _sum(self, what: str) -> int:
         total = 0
         for r in self.runners:
-            acc = r.engine.reduce(r.geom, r.bufs[r.cur], "hash", r.compute_stream)
+            acc = r.engine.reduce(r.geom, r.bufs[r.cur], what, r.compute_stream)
             r.compute_stream.synchronize()
             total = (total + int(acc.item())) & 0xFFFFFFFFFFFFFFFF
-        return int(_lib.load().gol_hash_finalize(total, self.width, self.height))
+        return total
+
+    def hash(self) -> int:
+        return int(_lib.load().gol_hash_finalize(self._sum("hash"), self.width, self.height))
+
+    def population(self) -> int:
+        return self._sum("population")
 
 
 def _largest_k(n: int) -> int:

@@ -122,16 +122,22 @@ int gol_layout(gol_board* b, int* ilv, int64_t* pitch);
 int gol_default_ilv(int64_t width);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
-/* Step-kernel decomposition the engine uses for a row of `width` cells in layout `ilv` at depth k:
- * the number of waves in a full-row workgroup (the row's blocks spread over one workgroup, block edges
- * exchanged through LDS), or 0 for per-wave column strips. */
-int gol_fullrow_wg(int64_t width, int ilv, int k);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller (multi-GPU
  * boards: strip 0's compute stream, which every pass joins at its end). */
 int gol_stream(gol_board* b, void** stream);
 
+/* Profiling: advance the board by ONE pass of its temporal depth with HIP timing events and report, per
+ * row strip (n = gol_num_parts), the microseconds from the pass start to the end of the interior launch
+ * (interior_us), to the release of the edge-band stream once the neighbours' halo rows have landed
+ * (wait_us: the edge-band wait) and to the end of the edge bands (edge_us).  A single board reports its
+ * one launch in interior_us and edge_us and 0 in wait_us.  Counts toward gol_generation. */
+int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, double* edge_us);
+
 const char* gol_last_error(void);
 const char* gol_version(void);
+/* 1 if a device reporting this hipDeviceProp_t::gcnArchName ("gfx950", "gfx950:sramecc+:xnack-") runs this
+ * build, else 0.  gol_create returns GOL_ERR_NO_DEVICE for a board on any other device. */
+int gol_arch_supported(const char* gcn_arch_name);
 
 /* ------------------------------------------------------------------------------------------------
  * Row-strip entry points for multi-GPU runs (one process per GPU; the caller owns device memory and

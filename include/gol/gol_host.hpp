@@ -21,6 +21,7 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <exception>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -211,16 +212,30 @@ class GameOfLife {  // what run() returns: IDisposable
         applyGrid([&](int x, int y) { agent_.post(UpdateView::update(cells[(size_t)(x + y * g.Width)] != 0, {x, y})); },
                   g);
     }
-    // L38-40: a timer calling updateView every period
+    // L38-40: a timer calling updateView every period.  A failed tick stops the timer and is kept for
+    // lastError() (an exception escaping the thread would terminate the process; the .NET timer handler of
+    // the reference does not bring the process down either).
     void start(std::chrono::milliseconds period) {
         timer_ = std::thread([this, period] {
             std::unique_lock<std::mutex> lk(stop_mu_);
             while (!stop_cv_.wait_for(lk, period, [this] { return stop_; })) {
                 lk.unlock();
-                updateView();
+                try {
+                    updateView();
+                } catch (...) {
+                    lk.lock();
+                    error_ = std::current_exception();
+                    stop_ = true;
+                    break;
+                }
                 lk.lock();
             }
         });
+    }
+    // the exception of the tick that stopped the timer, or nullptr
+    std::exception_ptr lastError() {
+        std::lock_guard<std::mutex> lk(stop_mu_);
+        return error_;
     }
     void Dispose() {
         {
@@ -238,6 +253,7 @@ class GameOfLife {  // what run() returns: IDisposable
     Emit emit_;
     std::mutex tick_;
     std::thread timer_;
+    std::exception_ptr error_;
     std::mutex stop_mu_;
     std::condition_variable stop_cv_;
     bool stop_ = false;

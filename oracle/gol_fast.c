@@ -48,6 +48,27 @@ int64_t fast_population(const uint64_t* b, int64_t W, int64_t H) {
     return p;
 }
 
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+/* oracle_seed_splitmix (gol_oracle.c) written straight into the 64-cell words: cells 64j .. 64j + 31 are
+ * the low 32 bits of splitmix64(seed ^ (y*W/32 + 2j)), cells 64j + 32 .. 64j + 63 those of 2j + 1. */
+int fast_seed_splitmix(uint64_t* board, int64_t W, int64_t H, uint64_t seed) {
+    if (!board || W < 64 || W % 64 || H < 1) return -1;
+    const int64_t nw = W / 64, wc = W / 32;
+    for (int64_t y = 0; y < H; y++)
+        for (int64_t j = 0; j < nw; j++) {
+            const uint64_t lo = (uint32_t)splitmix64(seed ^ (uint64_t)(y * wc + 2 * j));
+            const uint64_t hi = (uint32_t)splitmix64(seed ^ (uint64_t)(y * wc + 2 * j + 1));
+            board[y * nw + j] = lo | (hi << 32);
+        }
+    return 0;
+}
+
 /* full adder on bit planes */
 #define FA(a, b, c, s, co)                 \
     do {                                   \

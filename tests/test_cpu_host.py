@@ -59,6 +59,17 @@ def test_library_reports_version_without_gpu():
     assert b"gfx950" in _lib.load().gol_version()
 
 
+def test_arch_check_accepts_only_gfx950():
+    """gol_create refuses a board on a non-gfx950 device with GOL_ERR_NO_DEVICE (gol.h): the check's
+    decision on the device's gcnArchName, host code, exercised without a GPU."""
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    for name, ok in ((b"gfx950", 1), (b"gfx950:sramecc+:xnack-", 1), (b"gfx942", 0), (b"gfx942:sramecc+:xnack-", 0),
+                     (b"gfx9500", 0), (b"gfx90a", 0), (b"", 0), (None, 0)):
+        assert lib.gol_arch_supported(name) == ok, name
+
+
 def test_hash_finalize_matches_oracle(oracle):
     """gol_hash_finalize is host code: the product's final mix equals the oracle's."""
     from gameoflifewithactors_amd import hash_finalize

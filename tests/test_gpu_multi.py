@@ -135,3 +135,28 @@ def test_num_gpus_beyond_visible_devices_is_rejected(gol):
     if n >= 2:  # a real multi-GPU node: strips on devices 0..n-1 over xGMI
         with gol.Board(256, 128, 0, num_gpus=n) as b:
             assert [p["device"] for p in b.parts()] == list(range(n))
+
+
+def test_calls_restore_the_callers_device(gol, oracle):
+    """Every C-ABI call switches to the board's device and back (gol_capi.cpp DeviceGuard): a caller whose
+    current device is 1 keeps device 1 across create / step / readback / destroy of boards on device 0."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    b0 = _rand(64, 256, 5)
+    torch.cuda.set_device(1)
+    try:
+        for devices in ([0], [0, 0]):
+            with gol.Board(256, 64, devices=devices) as b:
+                assert torch.cuda.current_device() == 1
+                b.set_cells(b0).step(9)
+                assert torch.cuda.current_device() == 1
+                np.testing.assert_array_equal(b.get_cells(), oracle.run(b0, 9, 0))
+                b.hash(), b.population(), b.render_gray8()
+                assert torch.cuda.current_device() == 1
+            assert torch.cuda.current_device() == 1
+        x = torch.zeros(4, device="cuda")
+        assert x.device.index == 1
+    finally:
+        torch.cuda.set_device(0)

@@ -307,47 +307,6 @@ def test_long_run_checkpoints(gol, oracle, name, tblock):
         assert b.generation == case["generations"]
 
 
-# ---------------------------------------------------------------- full-row workgroup mode
-_FULLROW_SCRIPT = r"""
-import json, os, sys
-import numpy as np
-root = os.environ["GOL_TEST_ROOT"]
-sys.path[:0] = [root, os.path.join(root, "oracle")]
-import gameoflifewithactors_amd as g
-import gol_oracle as o
-from gameoflifewithactors_amd import _lib
-lib = _lib.load()
-out = []
-for boundary in (0, 1):
-    for ilv, k, h in ((4, 4, 40), (4, 8, 300), (2, 8, 300)):
-        wg = lib.gol_fullrow_wg(65536, ilv, k)
-        b0 = (np.random.default_rng(ilv * 100 + k + boundary).random((h, 65536)) < 0.4).astype(np.uint8)
-        gens = 2 * k + 3
-        with g.Board(65536, h, boundary, tblock_k=k, ilv=ilv) as b:
-            b.set_cells(b0).step(gens)
-            ok = bool(np.array_equal(b.get_cells(), o.c_run(b0, gens, boundary)))
-        out.append([boundary, ilv, k, wg, ok])
-print(json.dumps(out))
-"""
-
-
-def test_fullrow_workgroup_mode_matches_oracle():
-    """Full-row workgroups (GOL_FULLROW=1: a 65536-cell row spread over one workgroup, edges through LDS)
-    against the oracle, torus and bounded, every instantiated (ilv, k), in a child process so the mode
-    switch takes effect."""
-    import json
-    import subprocess
-    import sys
-
-    root = os.path.dirname(HERE)
-    env = dict(os.environ, GOL_FULLROW="1", GOL_TEST_ROOT=root)
-    r = subprocess.run([sys.executable, "-c", _FULLROW_SCRIPT], capture_output=True, text=True, timeout=150, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert all(wg > 0 for _, _, _, wg, _ in res), res
-    assert all(ok for *_, ok in res), res
-
-
 _SPLIT_SCRIPT = r"""
 import json, os, sys
 import numpy as np
