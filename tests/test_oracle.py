@@ -222,6 +222,43 @@ def test_fast_oracle_matches_byte_oracle(oracle, boundary, w, h, threads):
     assert marks[3][1:] == (oracle.board_hash(mid), oracle.population(mid))
 
 
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_full_size_generator_matches_byte_oracle(oracle, boundary):
+    """oracle/gol_fast_gen (which wrote tests/golden/golden_full.json) on a small board: its packed splitmix
+    seeding and every checkpoint equal the byte-per-cell oracle's."""
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "oracle", "build", "gol_fast_gen")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(root, "oracle"), "build/gol_fast_gen"], check=True,
+                       stdout=subprocess.DEVNULL)
+    w, h, seed = 320, 96, 0x5EED
+    out = subprocess.run([exe, str(w), str(h), str(boundary), str(seed), "60", "20", "3"], check=True,
+                         capture_output=True, text=True).stdout
+    marks = [json.loads(line) for line in out.splitlines()]
+    b = oracle.c_seed_splitmix(w, h, seed)
+    for m, gen in zip(marks, (0, 20, 40, 60)):
+        assert m["generation"] == gen
+        assert (m["hash"], m["population"]) == (oracle.board_hash(b), oracle.population(b)), gen
+        b = oracle.c_run(b, 20, boundary)
+
+
+def test_full_size_golden_is_consistent():
+    """golden_full.json: every case starts from the splitmix board and has a checkpoint per interval."""
+    import json
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_full.json")) as f:
+        full = json.load(f)
+    assert {"n1_65536_torus", "n1_65536_bounded", "c4_262144_torus"} <= set(full)
+    for c in full.values():
+        gens = [m[0] for m in c["checkpoints"]]
+        assert gens == list(range(0, c["generations"] + 1, c["every"]))
+    # torus and bounded start from the same seeded board
+    assert full["n1_65536_torus"]["checkpoints"][0] == full["n1_65536_bounded"]["checkpoints"][0]
+
+
 def test_fast_oracle_known_answers(oracle):
     b = np.zeros((1024, 1024), np.uint8)
     oracle.place_rle(b, oracle.R_PENTOMINO, 511, 511)
