@@ -77,6 +77,8 @@ def parse():
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="CPU baseline sample length (C2 actor sample, fair-CPU sample)")
+    p.add_argument("--cpu-c2", type=int, default=4096,
+                   help="board side of the C2 actor sample (BASELINE config 2: 4096; smaller for quick checks)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="N > 1: nccl (= RCCL over xGMI, the product path) or gloo (host-staged halo; lets "
@@ -128,14 +130,15 @@ def cpu_baseline(args):
         r = _run_json([exe, "100", "100", "100", str(threads), str(seed), "0", "dotnet-mod2"])
         c1[str(seed)] = {"gcups": r["cell_updates_per_s"] / 1e9, "seconds": round(r["seconds"], 3),
                          "generations": r["generations"], "messages": r["messages"], "hash": str(r["hash"])}
-    c2 = _run_json([exe, "4096", "4096", "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"])
+    n2 = str(args.cpu_c2)
+    c2 = _run_json([exe, n2, n2, "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"])
     fair = _run_json([fast, str(args.width), str(args.width), "0", str(threads), str(args.cpu_seconds)])
     return {
         "value": c2["cell_updates_per_s"] / 1e9,
         "unit": "GCUPS",
         "cores": threads,
         "kind": "port",
-        "sample": f"actor-protocol restatement (oracle/actor_protocol.cpp), C2 4096x4096 torus, dotnet-mod2 seed "
+        "sample": f"actor-protocol restatement (oracle/actor_protocol.cpp), C2 {n2}x{n2} torus, dotnet-mod2 seed "
         f"42, {c2['generations']} generation(s) in {c2['seconds']:.1f} s, {c2['messages']} messages, {threads} "
         f"threads on {cpu}",
         "c1_100x100_100gens": {

@@ -319,8 +319,27 @@ int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
     return GOL_OK;
 }
 
+// Boards small enough for one wavefront's registers (gol_wave.hip: W <= 128, H <= 256) run every gol_step call
+// as one single-wave launch; GOL_WAVE_RESIDENT=0 disables it (A/B runs), read on every call.
+bool use_wave_resident(const gol_board* b) {
+    const char* e = std::getenv("GOL_WAVE_RESIDENT");
+    if (e && e[0] == '0') return false;
+    return gol::wave_resident_rpl(b->W, b->H) > 0 && (!b->packed || b->ilv == 1);
+}
+
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
+    if (gens > 0 && use_wave_resident(b)) {
+        while (gens > 0) {
+            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
+            GOL_HIP(gol::launch_wave_resident(b->buf[b->cur], b->buf[b->cur ^ 1], b->W, b->H, b->pitch, g,
+                                              b->boundary == GOL_BOUNDED, !b->packed, b->stream));
+            b->cur ^= 1;
+            b->generation += g;
+            gens -= g;
+        }
+        return GOL_OK;
+    }
     if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
         (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
         const bool bounded = b->boundary == GOL_BOUNDED;

@@ -58,6 +58,15 @@ __device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
 }
+// GOL_XLANE_STAGED (staged deep levels only, whose exchanges are issued one row pair ahead of their use):
+// 0 = DPP both directions; 1 = the right-hand words by ds_bpermute_b32 (LDS pipe, no VALU slot), the left by
+// DPP; 2 = both by ds_bpermute_b32.
+#ifndef GOL_XLANE_STAGED
+#define GOL_XLANE_STAGED 0
+#endif
+__device__ __forceinline__ uint32_t bperm(int byte_addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(byte_addr, (int)v);
+}
 
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
 // into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
@@ -205,6 +214,8 @@ struct StreamWave {
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
                                           int64_t sx, int64_t sy, int role = -1)
         : src(s), dst(d), a(args) {
+        left_addr = ((lane - 1) & 63) * 4;
+        right_addr = ((lane + 1) & 63) * 4;
         const int64_t nblocks = a.words / M;
         // this lane's block column (may be off-board)
         const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
@@ -307,6 +318,26 @@ struct StreamWave {
         }
     }
 
+    // Block-edge words of rows a, b from the neighbouring lanes (GOL_XLANE_STAGED)
+    int left_addr = 0, right_addr = 0;  // ds_bpermute byte addresses of lanes i-1, i+1
+    __device__ __forceinline__ void xchg(const uint32_t (&pa)[M], const uint32_t (&pb)[M], uint32_t& la, uint32_t& lb,
+                                         uint32_t& ra, uint32_t& rb) const {
+        if (GOL_XLANE_STAGED >= 1) {
+            ra = bperm(right_addr, pa[0]);
+            rb = bperm(right_addr, pb[0]);
+        } else {
+            ra = from_right(pa[0]);
+            rb = from_right(pb[0]);
+        }
+        if (GOL_XLANE_STAGED >= 2) {
+            la = bperm(left_addr, pa[M - 1]);
+            lb = bperm(left_addr, pb[M - 1]);
+        } else {
+            la = from_left(pa[M - 1]);
+            lb = from_left(pb[M - 1]);
+        }
+    }
+
     // One level over a row pair (a = row r, b = row r+1 at level g), the same arithmetic as two level_row
     // calls, in a fixed interleaved order: fenced stages of independent instructions from the four chains
     // (2 rows x the block's first / other words), so no instruction issues right behind its producer.  The
@@ -314,24 +345,23 @@ struct StreamWave {
     // then depend on the instruction just before them, a single wave's dependent-issue latency).
     //   window on entry: X = sums of row r-2, Y = row r-1, aY = raw row r-1; on exit X = row r, Y = row r+1,
     //   aY = raw row r+1; oa / ob = generation g+1 of rows r-1 / r.
-    // pf: also issue the right-hand exchange of two more rows (pf_src -> pf_dst) in the first stage, for the
-    // next pair of this level or the first pair of the next level (see process).
-    __device__ __forceinline__ void pair_level(const uint32_t (&va)[M], const uint32_t (&vb)[M], uint32_t ra,
-                                               uint32_t rb, uint32_t (&sX)[M], uint32_t (&cX)[M], uint32_t (&sY)[M],
-                                               uint32_t (&cY)[M], uint32_t (&aY)[M], uint32_t ma, uint32_t mb,
-                                               uint32_t (&oa)[M], uint32_t (&ob)[M], bool pf, uint32_t pf_src0,
-                                               uint32_t pf_src1, uint32_t& pf_dst0, uint32_t& pf_dst1) {
+    // la / lb, ra / rb: the left lane's last word and the right lane's first word of rows a and b, exchanged
+    // one pair ahead.  pf: also issue the exchanges of two more rows (pa, pb: rows r+2, r+3 of this level or
+    // rows 0, 1 of the next; see process) in the first stage.
+    __device__ __forceinline__ void pair_level(const uint32_t (&va)[M], const uint32_t (&vb)[M], uint32_t la,
+                                               uint32_t lb, uint32_t ra, uint32_t rb, uint32_t (&sX)[M],
+                                               uint32_t (&cX)[M], uint32_t (&sY)[M], uint32_t (&cY)[M],
+                                               uint32_t (&aY)[M], uint32_t ma, uint32_t mb, uint32_t (&oa)[M],
+                                               uint32_t (&ob)[M], bool pf, const uint32_t (&pa)[M],
+                                               const uint32_t (&pb)[M], uint32_t& pla, uint32_t& plb, uint32_t& pra,
+                                               uint32_t& prb) {
 #define GOL_STAGE() __builtin_amdgcn_sched_barrier(0)
         uint32_t sa[M], ca[M], sb[M], cb[M];                 // row sums of rows r, r+1
         uint32_t A0[M], B0[M], X0[M], Y0[M], A1[M], B1[M], X1[M], Y1[M];  // vertical adds
         uint32_t p0[M], q0[M], p1[M], q1[M];                 // rule LUT tree, first level
         // 1: east funnel shifts (the right-hand words arrived early), west neighbours of the first words
         const uint32_t ea = align_right(ra, va[0], 1), eb = align_right(rb, vb[0], 1);
-        const uint32_t la = from_left(va[M - 1]), lb = from_left(vb[M - 1]);
-        if (pf) {
-            pf_dst0 = from_right(pf_src0);
-            pf_dst1 = from_right(pf_src1);
-        }
+        if (pf) xchg(pa, pb, pla, plb, pra, prb);
         GOL_STAGE();
         // 2: row sums of the words whose west neighbour is in the lane (j >= 1)
 #pragma unroll
@@ -455,9 +485,13 @@ struct StreamWave {
         // scheduling barrier separates the levels: without it the scheduler interleaves levels and the
         // live register set grows past the occupancy steps (K = 16, M = 2: 256 VGPRs, 1 wave/SIMD; with
         // it 213, 2 waves/SIMD; profiles/r1/ab_early.log, ab_fence2.log).
-        uint32_t right[R];
+        uint32_t right[R], left[R];
+        if (GOL_STAGED) {
+            xchg(v[0], v[1], left[0], left[1], right[0], right[1]);
+        } else {
 #pragma unroll
-        for (int r = 0; r < (GOL_STAGED ? 2 : R); r++) right[r] = from_right(v[r][0]);
+            for (int r = 0; r < R; r++) right[r] = from_right(v[r][0]);
+        }
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
@@ -477,8 +511,9 @@ struct StreamWave {
                     // the instruction that wrote the word (a DPP read needs 2 wait states after a VALU write)
                     const bool last = r + 2 >= R;
                     const int pr = last ? 0 : r + 2;
-                    pair_level(v[r], v[r + 1], right[r], right[r + 1], sX[g], cX[g], sY[g], cY[g], aY[g], m0, m1, o0,
-                               o1, !last || g + 1 < K, v[pr][0], v[pr + 1][0], right[pr], right[pr + 1]);
+                    pair_level(v[r], v[r + 1], left[r], left[r + 1], right[r], right[r + 1], sX[g], cX[g], sY[g],
+                               cY[g], aY[g], m0, m1, o0, o1, !last || g + 1 < K, v[pr], v[pr + 1], left[pr],
+                               left[pr + 1], right[pr], right[pr + 1]);
 #pragma unroll
                     for (int j = 0; j < M; j++) {
                         v[r][j] = o0[j];

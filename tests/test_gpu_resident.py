@@ -76,3 +76,51 @@ def test_resident_byte_input_values_normalised(gol, oracle):
     b0 = _rand(h, w, 99) * np.uint8(255)
     got = _run(gol, b0, 0, [5], resident=True)
     np.testing.assert_array_equal(got, oracle.run((b0 != 0).astype(np.uint8), 5, 0))
+
+
+# ---------------------------------------------------------------- single-wave register-resident pass
+def _run_wave(gol, b0, boundary, steps, wave):
+    h, w = b0.shape
+    old = os.environ.get("GOL_WAVE_RESIDENT")
+    os.environ["GOL_WAVE_RESIDENT"] = "1" if wave else "0"
+    try:
+        with gol.Board(w, h, boundary) as b:
+            b.set_cells(b0)
+            for g in steps:
+                b.step(g)
+            assert b.generation == sum(steps)
+            return b.get_cells()
+    finally:
+        if old is None:
+            os.environ.pop("GOL_WAVE_RESIDENT", None)
+        else:
+            os.environ["GOL_WAVE_RESIDENT"] = old
+
+
+# ragged (byte boards) and packed widths up to 128, heights up to 256 with 1-4 rows per lane; the
+# reference's own 100 x 100 board first (GameOfLifeLogic.fs:5)
+WAVE_SHAPES = [(100, 100), (3, 3), (5, 4), (33, 17), (97, 99), (127, 64), (128, 128), (64, 200), (32, 256),
+               (100, 3), (31, 192), (65, 130)]
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", WAVE_SHAPES)
+def test_wave_resident_matches_oracle_and_other_paths(gol, oracle, w, h, boundary):
+    b0 = _rand(h, w, 11 * w + h + boundary, p=0.4)
+    steps = [1, 40, 0, 59]
+    want = oracle.run(b0, sum(steps), boundary)
+    np.testing.assert_array_equal(_run_wave(gol, b0, boundary, steps, wave=True), want)
+    np.testing.assert_array_equal(_run_wave(gol, b0, boundary, steps, wave=False), want)
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_wave_resident_long_run_reference_board(gol, oracle, boundary):
+    """The reference's board, .NET Random seed 42 in its order (GameOfLifeDriver.fs:9-19), 5000 generations
+    in one call, against the C oracle."""
+    b0 = oracle.seed_dotnet(100, 100, 42, 0)
+    np.testing.assert_array_equal(_run_wave(gol, b0, boundary, [5000], wave=True), oracle.c_run(b0, 5000, boundary))
+
+
+def test_wave_resident_byte_values_normalised(gol, oracle):
+    b0 = _rand(100, 100, 3) * np.uint8(77)
+    np.testing.assert_array_equal(_run_wave(gol, b0, 0, [3], wave=True), oracle.run((b0 != 0).astype(np.uint8), 3, 0))

@@ -126,6 +126,11 @@ def test_bench_two_ranks_over_gloo():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["config"]["height"] == 2 * 4096
+    assert abs(r["value_per_gpu"] - r["value"] / 2) < 1e-2
+    # the one-process C-ABI leg (gol_create_multi, 2 strips on this GPU) ran after the main leg
+    h = r["handle_leg"]
+    assert h["value"] > 0 and h["strips"] == 2 and len(h["pass_timing_us"]) == 2, h
+    assert all(t["edge_done_us"] >= t["edge_wait_us"] >= 0 for t in h["pass_timing_us"])
 
 
 def test_262144_board_strips_match_single_board():
@@ -159,7 +164,7 @@ def test_bench_single_gpu_json_contract():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "4", "--warmup", "1", "--height", "8192",
-           "--cpu-seconds", "1", "--cpu-board", "64"]
+           "--cpu-seconds", "1", "--cpu-c2", "128"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=root)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -174,3 +179,5 @@ def test_bench_single_gpu_json_contract():
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     cb = r["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "GCUPS" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
+    assert set(cb["c1_100x100_100gens"]["gcups_by_seed"]) == {"0", "1", "42"} and cb["fair_cpu"]["value"] > 0
+    assert r["value_per_gpu"] == r["value"]
