@@ -27,7 +27,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# depths compared by the opt-in on-box autotune (--autotune), per layout (ilv)
+# depths raced on the box before the timed region (default; --no-autotune skips it), per layout (ilv)
 AUTOTUNE = {2: [12, 16], 1: [24, 32]}
 
 
@@ -71,8 +71,9 @@ def parse():
                    "262144); overrides --width/--height")
     p.add_argument("--tblock", type=int, default=0,
                    help="generations per pass (0 = the engine's default for the board layout)")
-    p.add_argument("--autotune", action="store_true",
-                   help="time the AUTOTUNE depths on the box and keep the faster (agreed across ranks)")
+    p.add_argument("--no-autotune", action="store_true",
+                   help="skip the on-box race between the AUTOTUNE depths (default: race them during warmup, "
+                   "interleaved, and time the faster; agreed across ranks) and use the engine default depth")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
     p.add_argument("--cpu-seconds", type=float, default=8.0,
@@ -234,11 +235,11 @@ def main():
         W, H = args.width, args.height * world
     lib = _lib.load()
     ilv = lib.gol_default_ilv(W)
-    # Temporal depth: --tblock, the fixed default, or (--autotune) a short on-box race between the depths
+    # Temporal depth: --tblock, the engine default (--no-autotune), or by default a short on-box race between the depths
     # that are within a few percent of each other across MI355X boxes.
     if args.tblock:
         cands = [args.tblock]
-    elif args.autotune:
+    elif not args.no_autotune:
         cands = AUTOTUNE.get(ilv, [default_depth(lib, ilv, world, args.boundary)])
     else:
         cands = [default_depth(lib, ilv, world, args.boundary)]
@@ -246,16 +247,18 @@ def main():
     runner.seed_splitmix(args.seed)
     k, tune = cands[0], None
     if len(cands) > 1:
-        per_gen = []
-        for kk in cands:
-            runner.step_pass(kk)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(runner.compute_stream)
-            for _ in range(4):
+        # interleaved rounds (the board and the clock drift during the race), best round per depth
+        per_gen = [float("inf")] * len(cands)
+        for _ in range(3):
+            for i, kk in enumerate(cands):
                 runner.step_pass(kk)
-            e1.record(runner.compute_stream)
-            torch.cuda.synchronize()
-            per_gen.append(e0.elapsed_time(e1) / (4 * kk))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(runner.compute_stream)
+                for _ in range(2):
+                    runner.step_pass(kk)
+                e1.record(runner.compute_stream)
+                torch.cuda.synchronize()
+                per_gen[i] = min(per_gen[i], e0.elapsed_time(e1) / (2 * kk))
         if world > 1:  # every rank must use the same depth (ghost rows, halo messages)
             t = torch.tensor(per_gen, dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -166,6 +166,11 @@ constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
+// Cooperative LDS-band pass (gol_coop.hip) for packed ilv-1 boards above the LDS-resident cut-over and below
+// this many cells; GOL_COOP=0 disables it, GOL_COOP_MAX_CELLS moves the cut-over (A/B runs; read per call).
+constexpr int64_t kCoopMaxCells = (int64_t)1 << 25;
+constexpr int kCoopFlagWords = 1024;            // flags of up to 1023 bands ...
+constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
 
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
@@ -210,6 +215,7 @@ struct gol_board {
     void* buf[2] = {nullptr, nullptr};
     int cur = 0;
     unsigned long long* acc = nullptr;  // device scratch accumulator
+    unsigned* coop = nullptr;           // cooperative pass: per-band flags + error word (allocated on first use)
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -245,6 +251,12 @@ int check_board(gol_board* b) {
 int sync(gol_board* b) {
     if (b->multi) return b->multi->synchronize();
     GOL_HIP(hipStreamSynchronize(b->stream));
+    if (b->coop) {  // a cooperative pass whose neighbour wait timed out left a wrong board: report it
+        int err = 0;
+        GOL_HIP(hipMemcpy(&err, b->coop + kCoopErrWord, sizeof(int), hipMemcpyDeviceToHost));
+        if (err) return fail(GOL_ERR_HIP, "cooperative pass: a band hand-off timed out (were other kernels "
+                                          "occupying CUs?); the board is invalid");
+    }
     return GOL_OK;
 }
 
@@ -327,6 +339,16 @@ bool use_wave_resident(const gol_board* b) {
     return gol::wave_resident_rpl(b->W, b->H) > 0 && (!b->packed || b->ilv == 1);
 }
 
+bool use_coop(const gol_board* b) {
+    const char* e = std::getenv("GOL_COOP");
+    if (e && e[0] == '0') return false;
+    const char* m = std::getenv("GOL_COOP_MAX_CELLS");
+    const int64_t maxc = m ? (int64_t)std::atoll(m) : kCoopMaxCells;
+    int nwg = 0, B = 0;
+    return b->packed && b->ilv == 1 && b->W * b->H <= maxc && gol::coop_plan(b->W, b->H, gol::coop_k(), &nwg, &B) &&
+           nwg < kCoopFlagWords;
+}
+
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
     if (gens > 0 && use_wave_resident(b)) {
@@ -354,6 +376,23 @@ int step_impl(gol_board* b, int64_t gens) {
                 GOL_HIP(gol::launch_resident_bytes(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H, g, bounded,
                                                    b->stream));
             b->cur ^= 1;
+            b->generation += g;
+            gens -= g;
+        }
+        return GOL_OK;
+    }
+    if (gens > 0 && use_coop(b)) {
+        if (!b->coop) {
+            GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
+            GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
+        }
+        while (gens > 0) {
+            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
+            GOL_HIP(gol::launch_coop_pass(b->words(0), b->words(1), b->cur, b->W, b->H, b->pitch, g,
+                                          b->boundary == GOL_BOUNDED, b->coop,
+                                          reinterpret_cast<int*>(b->coop + kCoopErrWord), b->stream));
+            const int64_t k = gol::coop_k();
+            if (((g + k - 1) / k) % 2) b->cur ^= 1;  // each block of <= k generations flips the buffers
             b->generation += g;
             gens -= g;
         }
@@ -405,6 +444,7 @@ void free_board(gol_board* b) {
     for (auto& p : b->buf)
         if (p) (void)hipFree(p);
     if (b->acc) (void)hipFree(b->acc);
+    if (b->coop) (void)hipFree(b->coop);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }

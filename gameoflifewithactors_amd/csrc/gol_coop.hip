@@ -1,0 +1,223 @@
+// gol_coop.hip -- persistent, LDS-banded pass for mid-size boards (BASELINE config 2: 4096^2) on gfx950.
+//
+// A 4096^2 board is 2 MiB packed: too large for one CU's LDS (gol_resident.hip), too small to fill the chip
+// with the streaming pass (gol_step.hip), where each wave is one long serial chain per launch.  Here ONE
+// workgroup per CU stays resident for a whole gol_step call and owns a band of B rows.  Per block of k
+// generations (k <= K, B >= k) it
+//   1. loads its band plus k halo rows on each side (rows wrap on a torus, GameOfLifeDriver.fs:21-25; rows
+//      beyond a bounded board are dead, Script.fsx:6-13) from the board buffer into LDS,
+//   2. runs k synchronous B3/S23 generations (GameOfLifeLogic.fs:59-63) between two LDS buffers with one
+//      workgroup barrier per generation (the halo shrinks by a row per generation; the band stays exact),
+//   3. stores its band to the other board buffer and publishes "block done" to its two neighbours,
+// and before the next block waits only for its two neighbour bands (their halo rows, and that they have
+// finished reading the rows it is about to overwrite).  No grid barrier, one launch per call.
+//
+// Hand-off protocol (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility"): every wave's
+// stores drain (s_waitcnt vmcnt(0)), workgroup barrier, one lane: agent-scope release fence, s_waitcnt
+// vmcnt(0) (the compiler may drop the one after the fence), relaxed agent-scope store of the flag; the
+// consumer polls with relaxed agent-scope loads + s_sleep, then an agent-scope acquire fence and a workgroup
+// barrier before its plain loads.  Residency: the grid is one workgroup per CU, each asking for more than
+// half of the CU's LDS, launched cooperatively (the runtime rejects a grid that cannot be co-resident); every
+// spin is bounded and a timed-out wait raises an error word the host checks on the next synchronisation.
+#include "gol_internal.h"
+#include "gol_bitlogic.h"
+
+#include <cstdlib>
+
+namespace gol {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kMinLds = 96 * 1024;  // > half the CU's 160 KiB: one workgroup per CU
+constexpr unsigned kSpinLimit = 1u << 22;  // ~ seconds: a wait this long means a band is not resident
+
+struct CoopArgs {
+    uint32_t* buf[2];
+    int64_t pitch;   // words per buffer row
+    int wpr;         // words per board row (W / 32)
+    int H;           // board rows
+    int B;           // rows per band
+    int nwg;         // bands (= workgroups)
+    int K;           // generations per block (<= B)
+    int gens;
+    int cur;         // buffer holding the board at launch
+    unsigned* flags; // per band: blocks completed (zeroed before the launch)
+    int* err;        // set to 1 by a timed-out wait
+};
+
+// Horizontal 3-sums of word c of an LDS row (ilv-1 layout).
+template <bool BOUNDED>
+__device__ __forceinline__ uint32_t lds_row(const uint32_t* row, int wpr, int c, uint32_t& s, uint32_t& cy) {
+    const uint32_t m = row[c];
+    const uint32_t l = (BOUNDED && c == 0) ? 0u : row[c == 0 ? wpr - 1 : c - 1];
+    const uint32_t r = (BOUNDED && c == wpr - 1) ? 0u : row[c == wpr - 1 ? 0 : c + 1];
+    row_sum(l, m, r, s, cy);
+    return m;
+}
+
+__device__ __forceinline__ bool wait_flag(const unsigned* f, unsigned target) {
+    for (unsigned i = 0; i < kSpinLimit; i++) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+template <bool BOUNDED>
+__global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
+    extern __shared__ uint32_t lds[];
+    const int band = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int y0 = band * a.B;
+    const int y1 = y0 + a.B < a.H ? y0 + a.B : a.H;
+    const int own = y1 - y0;
+    const int wpr = a.wpr;
+    const int stride = (a.B + 2 * a.K) * wpr;  // words per LDS buffer
+    // neighbour bands (a bounded board's end bands have one; a one-band torus is its own neighbour)
+    const int up = band > 0 ? band - 1 : (BOUNDED ? -1 : a.nwg - 1);
+    const int dn = band + 1 < a.nwg ? band + 1 : (BOUNDED ? -1 : 0);
+    // column-segment items: `segs` row segments per column
+    const int segs = wpr >= kThreads ? 1 : kThreads / wpr;
+    const int items = wpr * segs;
+    int cur = a.cur;
+    const int nblk = (a.gens + a.K - 1) / a.K;
+    for (int blk = 0; blk < nblk; blk++) {
+        const int k = a.gens - blk * a.K < a.K ? a.gens - blk * a.K : a.K;
+        if (blk > 0) {  // the neighbours finished block blk - 1: their band rows are stored, our rows are read
+            if (tid == 0) {
+                bool ok = true;
+                if (up >= 0) ok = wait_flag(a.flags + up, (unsigned)blk) && ok;
+                if (dn >= 0) ok = wait_flag(a.flags + dn, (unsigned)blk) && ok;
+                if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+        }
+        // 1. band + k halo rows -> LDS buffer 0 (local row i = global row y0 - k + i)
+        const int n = own + 2 * k;
+        const uint32_t* src = a.buf[cur];
+        for (int i = tid; i < n * wpr; i += kThreads) {
+            const int r = i / wpr, c = i - r * wpr;
+            int gy = y0 - k + r;
+            uint32_t v = 0;
+            if (gy >= 0 && gy < a.H) {
+                v = src[(int64_t)gy * a.pitch + c];
+            } else if (!BOUNDED) {
+                gy = gy < 0 ? gy + a.H : gy - a.H;
+                v = src[(int64_t)gy * a.pitch + c];
+            }
+            lds[r * wpr + c] = v;
+        }
+        __syncthreads();
+        // 2. k generations in LDS: generation j writes local rows [j + 1, n - 1 - j)
+        uint32_t* A = lds;
+        uint32_t* Bf = lds + stride;
+        for (int j = 0; j < k; j++) {
+            const int r0 = j + 1, r1 = n - 1 - j, rows = r1 - r0;
+            for (int it = tid; it < items; it += kThreads) {
+                const int sg = it / wpr, c = it - sg * wpr;
+                const int ra = r0 + sg * rows / segs, rb = r0 + (sg + 1) * rows / segs;
+                if (ra >= rb) continue;
+                uint32_t sP, cP, sC, cC, sN, cN;
+                lds_row<BOUNDED>(A + (ra - 1) * wpr, wpr, c, sP, cP);
+                uint32_t mC = lds_row<BOUNDED>(A + ra * wpr, wpr, c, sC, cC);
+                for (int r = ra; r < rb; r++) {
+                    const uint32_t mN = lds_row<BOUNDED>(A + (r + 1) * wpr, wpr, c, sN, cN);
+                    uint32_t v = life_next(sP, cP, sC, cC, sN, cN, mC);
+                    if (BOUNDED) {
+                        const int gy = y0 - k + r;
+                        if (gy < 0 || gy >= a.H) v = 0u;  // dead outside the board at every generation
+                    }
+                    Bf[r * wpr + c] = v;
+                    sP = sC, cP = cC, sC = sN, cC = cN, mC = mN;
+                }
+            }
+            __syncthreads();
+            uint32_t* t = A;
+            A = Bf;
+            Bf = t;
+        }
+        // 3. the band (local rows [k, k + own)) -> the other buffer, then publish
+        uint32_t* dst = a.buf[cur ^ 1];
+        for (int i = tid; i < own * wpr; i += kThreads) {
+            const int r = i / wpr, c = i - r * wpr;
+            dst[(int64_t)(y0 + r) * a.pitch + c] = A[(k + r) * wpr + c];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        cur ^= 1;
+    }
+}
+
+int coop_cus() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 0;
+        return n;
+    }();
+    return cus;
+}
+
+}  // namespace
+
+// Generations per block: GOL_COOP_K overrides (A/B), default 8.
+int coop_k() {
+    const char* e = std::getenv("GOL_COOP_K");
+    const int k = e ? std::atoi(e) : 8;
+    return k >= 1 && k <= 64 ? k : 8;
+}
+
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B) {
+    const int cus = coop_cus();
+    if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1) return false;
+    const int64_t wpr = W / 32;
+    int64_t b = (H + cus - 1) / cus;
+    if (b < k) b = k;  // a halo of k rows comes from one neighbour band
+    const int64_t n = (H + b - 1) / b;
+    if (2 * (b + 2 * k) * wpr * 4 > 160 * 1024) return false;
+    *nwg = (int)n;
+    *B = (int)b;
+    return true;
+}
+
+hipError_t launch_coop_pass(uint32_t* buf0, uint32_t* buf1, int cur, int64_t W, int64_t H, int64_t pitch,
+                            int64_t gens, bool bounded, unsigned* flags, int* err, hipStream_t s) {
+    const int k = coop_k();
+    int nwg = 0, B = 0;
+    if (!coop_plan(W, H, k, &nwg, &B) || gens < 1 || gens > INT32_MAX || pitch < W / 32) return hipErrorInvalidValue;
+    CoopArgs a;
+    a.buf[0] = buf0;
+    a.buf[1] = buf1;
+    a.pitch = pitch;
+    a.wpr = (int)(W / 32);
+    a.H = (int)H;
+    a.B = B;
+    a.nwg = nwg;
+    a.K = k;
+    a.gens = (int)gens;
+    a.cur = cur;
+    a.flags = flags;
+    a.err = err;
+    const size_t need = (size_t)2 * (B + 2 * k) * a.wpr * 4;
+    const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
+    hipError_t e = hipMemsetAsync(flags, 0, (size_t)nwg * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    const void* fn = bounded ? (const void*)&gol_coop_pass<true> : (const void*)&gol_coop_pass<false>;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[bounded]) {
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set[bounded] = true;
+    }
+    void* args[] = {&a};
+    return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);
+}
+
+}  // namespace gol

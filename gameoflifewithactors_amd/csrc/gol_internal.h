@@ -71,6 +71,12 @@ hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W,
 hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, int64_t gens, bool bounded,
                                  hipStream_t s);
 
+// ---- gol_coop.hip: one workgroup per CU owning a band of rows in LDS, k generations per neighbour hand-off
+int coop_k();
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B);
+hipError_t launch_coop_pass(uint32_t* buf0, uint32_t* buf1, int cur, int64_t W, int64_t H, int64_t pitch,
+                            int64_t gens, bool bounded, unsigned* flags, int* err, hipStream_t s);
+
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
 int wave_resident_rpl(int64_t W, int64_t H);  // rows per lane, 0 = the board does not fit
 hipError_t launch_wave_resident(const void* src, void* dst, int64_t W, int64_t H, int64_t pitch, int64_t gens,

@@ -58,15 +58,6 @@ __device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
 }
-// GOL_XLANE_STAGED (staged deep levels only, whose exchanges are issued one row pair ahead of their use):
-// 0 = DPP both directions; 1 = the right-hand words by ds_bpermute_b32 (LDS pipe, no VALU slot), the left by
-// DPP; 2 = both by ds_bpermute_b32.
-#ifndef GOL_XLANE_STAGED
-#define GOL_XLANE_STAGED 0
-#endif
-__device__ __forceinline__ uint32_t bperm(int byte_addr, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(byte_addr, (int)v);
-}
 
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
 // into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
@@ -76,11 +67,6 @@ __device__ __forceinline__ uint32_t bperm(int byte_addr, uint32_t v) {
 #if GOL_STAMP
 static constexpr int kStamps = 1 << 16;
 __device__ unsigned long long g_stamps[2][kStamps];
-#endif
-// GOL_STAGED: deep levels in the fixed interleaved order of StreamWave::pair_level (1) or as two
-// compiler-scheduled level_row calls (0)
-#ifndef GOL_STAGED
-#define GOL_STAGED 1
 #endif
 // sched_barrier mask: every instruction class may cross except DS (0x80 all DS, 0x100 DS read, 0x200 DS write)
 static constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
@@ -214,8 +200,6 @@ struct StreamWave {
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
                                           int64_t sx, int64_t sy, int role = -1)
         : src(s), dst(d), a(args) {
-        left_addr = ((lane - 1) & 63) * 4;
-        right_addr = ((lane + 1) & 63) * 4;
         const int64_t nblocks = a.words / M;
         // this lane's block column (may be off-board)
         const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
@@ -318,137 +302,6 @@ struct StreamWave {
         }
     }
 
-    // Block-edge words of rows a, b from the neighbouring lanes (GOL_XLANE_STAGED)
-    int left_addr = 0, right_addr = 0;  // ds_bpermute byte addresses of lanes i-1, i+1
-    __device__ __forceinline__ void xchg(const uint32_t (&pa)[M], const uint32_t (&pb)[M], uint32_t& la, uint32_t& lb,
-                                         uint32_t& ra, uint32_t& rb) const {
-        if (GOL_XLANE_STAGED >= 1) {
-            ra = bperm(right_addr, pa[0]);
-            rb = bperm(right_addr, pb[0]);
-        } else {
-            ra = from_right(pa[0]);
-            rb = from_right(pb[0]);
-        }
-        if (GOL_XLANE_STAGED >= 2) {
-            la = bperm(left_addr, pa[M - 1]);
-            lb = bperm(left_addr, pb[M - 1]);
-        } else {
-            la = from_left(pa[M - 1]);
-            lb = from_left(pb[M - 1]);
-        }
-    }
-
-    // One level over a row pair (a = row r, b = row r+1 at level g), the same arithmetic as two level_row
-    // calls, in a fixed interleaved order: fenced stages of independent instructions from the four chains
-    // (2 rows x the block's first / other words), so no instruction issues right behind its producer.  The
-    // machine scheduler, left alone, emits each word's chain back to back (a fifth of the VALU instructions
-    // then depend on the instruction just before them, a single wave's dependent-issue latency).
-    //   window on entry: X = sums of row r-2, Y = row r-1, aY = raw row r-1; on exit X = row r, Y = row r+1,
-    //   aY = raw row r+1; oa / ob = generation g+1 of rows r-1 / r.
-    // la / lb, ra / rb: the left lane's last word and the right lane's first word of rows a and b, exchanged
-    // one pair ahead.  pf: also issue the exchanges of two more rows (pa, pb: rows r+2, r+3 of this level or
-    // rows 0, 1 of the next; see process) in the first stage.
-    __device__ __forceinline__ void pair_level(const uint32_t (&va)[M], const uint32_t (&vb)[M], uint32_t la,
-                                               uint32_t lb, uint32_t ra, uint32_t rb, uint32_t (&sX)[M],
-                                               uint32_t (&cX)[M], uint32_t (&sY)[M], uint32_t (&cY)[M],
-                                               uint32_t (&aY)[M], uint32_t ma, uint32_t mb, uint32_t (&oa)[M],
-                                               uint32_t (&ob)[M], bool pf, const uint32_t (&pa)[M],
-                                               const uint32_t (&pb)[M], uint32_t& pla, uint32_t& plb, uint32_t& pra,
-                                               uint32_t& prb) {
-#define GOL_STAGE() __builtin_amdgcn_sched_barrier(0)
-        uint32_t sa[M], ca[M], sb[M], cb[M];                 // row sums of rows r, r+1
-        uint32_t A0[M], B0[M], X0[M], Y0[M], A1[M], B1[M], X1[M], Y1[M];  // vertical adds
-        uint32_t p0[M], q0[M], p1[M], q1[M];                 // rule LUT tree, first level
-        // 1: east funnel shifts (the right-hand words arrived early), west neighbours of the first words
-        const uint32_t ea = align_right(ra, va[0], 1), eb = align_right(rb, vb[0], 1);
-        if (pf) xchg(pa, pb, pla, plb, pra, prb);
-        GOL_STAGE();
-        // 2: row sums of the words whose west neighbour is in the lane (j >= 1)
-#pragma unroll
-        for (int j = 1; j < M; j++) {
-            const uint32_t xa = j == M - 1 ? ea : va[j + 1], xb = j == M - 1 ? eb : vb[j + 1];
-            sa[j] = lut3<0x96>(va[j - 1], va[j], xa);
-            ca[j] = lut3<0xE8>(va[j - 1], va[j], xa);
-            sb[j] = lut3<0x96>(vb[j - 1], vb[j], xb);
-            cb[j] = lut3<0xE8>(vb[j - 1], vb[j], xb);
-        }
-        GOL_STAGE();
-        // 3: row r vertical sums, words j >= 1 (P = X, C = Y, N = row r)
-#pragma unroll
-        for (int j = 1; j < M; j++) {
-            A0[j] = lut3<0x96>(sX[j], sY[j], sa[j]);
-            B0[j] = lut3<0xE8>(sX[j], sY[j], sa[j]);
-            X0[j] = lut3<0x96>(cX[j], cY[j], ca[j]);
-            Y0[j] = lut3<0xE8>(cX[j], cY[j], ca[j]);
-        }
-        GOL_STAGE();
-        // 4: west funnel shifts; row r+1 vertical sums, words j >= 1 (P = Y, C = row r, N = row r+1)
-        const uint32_t wa = align_right(va[M - 1], la, 31), wb = align_right(vb[M - 1], lb, 31);
-#pragma unroll
-        for (int j = 1; j < M; j++) {
-            A1[j] = lut3<0x96>(sY[j], sa[j], sb[j]);
-            B1[j] = lut3<0xE8>(sY[j], sa[j], sb[j]);
-            X1[j] = lut3<0x96>(cY[j], ca[j], cb[j]);
-            Y1[j] = lut3<0xE8>(cY[j], ca[j], cb[j]);
-        }
-        GOL_STAGE();
-        // 5: row sums of the first words; row r rule, words j >= 1 (first level)
-        {
-            const uint32_t xa = M == 1 ? ea : va[1 % M], xb = M == 1 ? eb : vb[1 % M];
-            sa[0] = lut3<0x96>(wa, va[0], xa);
-            ca[0] = lut3<0xE8>(wa, va[0], xa);
-            sb[0] = lut3<0x96>(wb, vb[0], xb);
-            cb[0] = lut3<0xE8>(wb, vb[0], xb);
-        }
-#pragma unroll
-        for (int j = 1; j < M; j++) {
-            p0[j] = lut3<0x27>(A0[j], Y0[j], aY[j]);
-            q0[j] = lut3<0x19>(B0[j], X0[j], Y0[j]);
-        }
-        GOL_STAGE();
-        // 6: row r vertical sums of the first word; row r outputs j >= 1; row r+1 rule j >= 1
-        A0[0] = lut3<0x96>(sX[0], sY[0], sa[0]);
-        B0[0] = lut3<0xE8>(sX[0], sY[0], sa[0]);
-        X0[0] = lut3<0x96>(cX[0], cY[0], ca[0]);
-        Y0[0] = lut3<0xE8>(cX[0], cY[0], ca[0]);
-#pragma unroll
-        for (int j = 1; j < M; j++) {
-            oa[j] = lut3<0x24>(p0[j], q0[j], A0[j]);
-            p1[j] = lut3<0x27>(A1[j], Y1[j], va[j]);
-            q1[j] = lut3<0x19>(B1[j], X1[j], Y1[j]);
-        }
-        GOL_STAGE();
-        // 7: row r+1 vertical sums of the first word; row r rule word 0; row r+1 outputs j >= 1
-        A1[0] = lut3<0x96>(sY[0], sa[0], sb[0]);
-        B1[0] = lut3<0xE8>(sY[0], sa[0], sb[0]);
-        X1[0] = lut3<0x96>(cY[0], ca[0], cb[0]);
-        Y1[0] = lut3<0xE8>(cY[0], ca[0], cb[0]);
-        p0[0] = lut3<0x27>(A0[0], Y0[0], aY[0]);
-        q0[0] = lut3<0x19>(B0[0], X0[0], Y0[0]);
-#pragma unroll
-        for (int j = 1; j < M; j++) ob[j] = lut3<0x24>(p1[j], q1[j], A1[j]);
-        GOL_STAGE();
-        // 8: row r output word 0; row r+1 rule word 0
-        oa[0] = lut3<0x24>(p0[0], q0[0], A0[0]);
-        p1[0] = lut3<0x27>(A1[0], Y1[0], va[0]);
-        q1[0] = lut3<0x19>(B1[0], X1[0], Y1[0]);
-        GOL_STAGE();
-        ob[0] = lut3<0x24>(p1[0], q1[0], A1[0]);
-#pragma unroll
-        for (int j = 0; j < M; j++) {
-            if (BOUNDED) {
-                oa[j] &= ma;
-                ob[j] &= mb;
-            }
-            sX[j] = sa[j];
-            cX[j] = ca[j];
-            sY[j] = sb[j];
-            cY[j] = cb[j];
-            aY[j] = vb[j];
-        }
-#undef GOL_STAGE
-    }
-
     // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
     template <bool SKIP>
@@ -485,13 +338,9 @@ struct StreamWave {
         // scheduling barrier separates the levels: without it the scheduler interleaves levels and the
         // live register set grows past the occupancy steps (K = 16, M = 2: 256 VGPRs, 1 wave/SIMD; with
         // it 213, 2 waves/SIMD; profiles/r1/ab_early.log, ab_fence2.log).
-        uint32_t right[R], left[R];
-        if (GOL_STAGED) {
-            xchg(v[0], v[1], left[0], left[1], right[0], right[1]);
-        } else {
+        uint32_t right[R];
 #pragma unroll
-            for (int r = 0; r < R; r++) right[r] = from_right(v[r][0]);
-        }
+        for (int r = 0; r < R; r++) right[r] = from_right(v[r][0]);
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
@@ -505,31 +354,14 @@ struct StreamWave {
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-                if (GOL_STAGED) {
-                    // right-hand exchanges one pair ahead: rows r+2, r+3 of this level, or (last pair) rows 0, 1
-                    // of the next level, whose inputs pair 0 produced a whole pair ago -- never right behind
-                    // the instruction that wrote the word (a DPP read needs 2 wait states after a VALU write)
-                    const bool last = r + 2 >= R;
-                    const int pr = last ? 0 : r + 2;
-                    pair_level(v[r], v[r + 1], left[r], left[r + 1], right[r], right[r + 1], sX[g], cX[g], sY[g],
-                               cY[g], aY[g], m0, m1, o0, o1, !last || g + 1 < K, v[pr], v[pr + 1], left[pr],
-                               left[pr + 1], right[pr], right[pr + 1]);
+                level_row(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
+                          o1);
 #pragma unroll
-                    for (int j = 0; j < M; j++) {
-                        v[r][j] = o0[j];
-                        v[r + 1][j] = o1[j];
-                    }
-                    continue;
-                } else {
-                    level_row(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-                    level_row(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r],
-                              m1, o1);
-#pragma unroll
-                    for (int j = 0; j < M; j++) {
-                        aY[g][j] = v[r + 1][j];
-                        v[r][j] = o0[j];
-                        v[r + 1][j] = o1[j];
-                    }
+                for (int j = 0; j < M; j++) {
+                    aY[g][j] = v[r + 1][j];
+                    v[r][j] = o0[j];
+                    v[r + 1][j] = o1[j];
                 }
                 if (g + 1 < K) {
                     right[r] = from_right(o0[0]);

@@ -1,0 +1,92 @@
+"""GPU parity of the cooperative LDS-band pass for mid-size boards (csrc/gol_coop.hip).
+
+Packed boards above the LDS-resident cut-over (2^17 cells) and up to 2^25 cells run every gol_step call as one
+persistent launch: one workgroup per CU owns a band of rows in LDS and hands its edge rows to its two
+neighbour bands every k generations.  Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus
+GameOfLifeDriver.fs:21-25; bounded Script.fsx:6-13), the BASELINE config-2 golden checkpoints (4096^2, .NET
+Random seed 42, 10k generations), and the streaming pass on the same board (GOL_COOP=0).  Uneven bands
+(heights that do not divide over the CUs), several block depths (GOL_COOP_K) and split calls are covered.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def gol():
+    import gameoflifewithactors_amd as g
+    from gameoflifewithactors_amd import _lib
+
+    _lib.load()
+    return g
+
+
+def _rand(h, w, seed, p=0.45):
+    return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
+
+
+class _Env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _run(gol, b0, boundary, steps, coop, k=None):
+    h, w = b0.shape
+    env = {"GOL_COOP": "1" if coop else "0"}
+    if k:
+        env["GOL_COOP_K"] = str(k)
+    with _Env(**env), gol.Board(w, h, boundary) as b:
+        assert b.info()["ilv"] == 1
+        b.set_cells(b0)
+        for g in steps:
+            b.step(g)
+        assert b.generation == sum(steps)
+        return b.get_cells()
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", [(1024, 1024), (512, 2048), (2048, 300), (4096, 4096), (2016, 1500), (8192, 512)])
+def test_coop_matches_oracle_and_streaming(gol, oracle, w, h, boundary):
+    b0 = _rand(h, w, w + 3 * h + boundary)
+    steps = [1, 20, 0, 29]  # split calls; blocks of 8 plus remainders
+    want = oracle.c_run(b0, sum(steps), boundary)
+    np.testing.assert_array_equal(_run(gol, b0, boundary, steps, coop=True), want)
+    np.testing.assert_array_equal(_run(gol, b0, boundary, steps, coop=False), want)
+
+
+@pytest.mark.parametrize("k", [1, 3, 8, 16])
+def test_coop_block_depths(gol, oracle, k):
+    b0 = _rand(1024, 2048, 40 + k)
+    for boundary in (0, 1):
+        np.testing.assert_array_equal(_run(gol, b0, boundary, [37], coop=True, k=k), oracle.c_run(b0, 37, boundary))
+
+
+def test_coop_config2_golden_checkpoints(gol):
+    """BASELINE config 2: 4096^2 torus, .NET Random seed 42 in the reference's order, every checkpoint (hash +
+    population every 100 generations) to generation 10,000, on the cooperative pass."""
+    with open(os.path.join(HERE, "golden", "golden_long.json")) as f:
+        case = json.load(f)["c2_4096_torus_dotnet42"]
+    with _Env(GOL_COOP="1"), gol.Board(case["width"], case["height"], case["boundary"]) as b:
+        b.seed_dotnet(case["seed"], gol.INIT_DOTNET_MOD2)
+        done = 0
+        for gen, h, pop in case["checkpoints"]:
+            b.step(gen - done)
+            done = gen
+            assert (b.hash(), b.population()) == (h, pop), gen

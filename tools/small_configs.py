@@ -12,10 +12,12 @@ from gameoflifewithactors_amd import Board
 CASES = [(100, 100, 0, 100, 'dotnet'), (100, 100, 0, 10000, 'dotnet'), (100, 100, 1, 10000, 'dotnet'),
          (64, 64, 0, 20000, 'dotnet'), (128, 128, 1, 20000, 'dotnet'), (96, 192, 0, 20000, 'dotnet'), (4096, 4096, 0, 1000, 'dotnet'),
          (256, 256, 1, 100000, 'rle'), (128, 128, 0, 20000, 'dotnet'), (256, 256, 0, 20000, 'dotnet'),
-         (512, 256, 0, 10000, 'dotnet'), (512, 512, 0, 10000, 'dotnet'), (1024, 512, 0, 10000, 'dotnet'),
+         (512, 256, 0, 10000, 'dotnet'), (512, 512, 0, 10000, 'dotnet'), (1024, 512, 0, 10000, 'dotnet'), (1024, 1024, 0, 10000, 'dotnet'),
+         (2048, 2048, 0, 4000, 'dotnet'), (4096, 4096, 1, 1000, 'dotnet'), (8192, 4096, 0, 1000, 'dotnet'),
          (255, 257, 0, 10000, 'dotnet')]
 mode = os.environ.get("GOL_RESIDENT_MAX_CELLS", "default")
 wave = os.environ.get("GOL_WAVE_RESIDENT", "default")
+coop = os.environ.get("GOL_COOP", "default") + ":" + os.environ.get("GOL_COOP_K", "8")
 for (w, h, bnd, gens, seed) in CASES:
     with Board(w, h, bnd) as b:
         if seed == 'dotnet':
@@ -24,6 +26,6 @@ for (w, h, bnd, gens, seed) in CASES:
             b.place_rle("b2o$2o$bo!", w // 2, h // 2)
         b.step(2); b.synchronize()
         t0 = time.perf_counter(); b.step(gens); b.synchronize(); dt = time.perf_counter() - t0
-        print(json.dumps({"resident_max_cells": mode, "wave_resident": wave, "w": w, "h": h, "boundary": bnd, "gens": gens,
+        print(json.dumps({"resident_max_cells": mode, "wave_resident": wave, "coop": coop, "w": w, "h": h, "boundary": bnd, "gens": gens,
                           "ms": round(dt * 1e3, 3), "us_per_gen": round(dt / gens * 1e6, 3),
                           "gcups": round(w * h * gens / dt / 1e9, 2), "k": b.info()["tblock_k"]}), flush=True)
