@@ -36,7 +36,7 @@ struct CoopArgs {
     int64_t pitch;   // words per buffer row
     int wpr;         // words per board row (W / 32)
     int H;           // board rows
-    int B;           // rows per band
+    int B;           // rows of the largest band (LDS sizing)
     int nwg;         // bands (= workgroups)
     int K;           // generations per block (<= B)
     int gens;
@@ -68,8 +68,9 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
     extern __shared__ uint32_t lds[];
     const int band = blockIdx.x;
     const int tid = threadIdx.x;
-    const int y0 = band * a.B;
-    const int y1 = y0 + a.B < a.H ? y0 + a.B : a.H;
+    // balanced bands: every band has at least K rows, so a k-row halo comes from ONE neighbour band
+    const int y0 = (int)((int64_t)a.H * band / a.nwg);
+    const int y1 = (int)((int64_t)a.H * (band + 1) / a.nwg);
     const int own = y1 - y0;
     const int wpr = a.wpr;
     const int stride = (a.B + 2 * a.K) * wpr;  // words per LDS buffer
@@ -178,9 +179,10 @@ bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B) {
     const int cus = coop_cus();
     if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1) return false;
     const int64_t wpr = W / 32;
-    int64_t b = (H + cus - 1) / cus;
-    if (b < k) b = k;  // a halo of k rows comes from one neighbour band
-    const int64_t n = (H + b - 1) / b;
+    // balanced bands of >= k rows each (a k-row halo then comes from one neighbour band), one per CU at most
+    int64_t n = H / k < cus ? H / k : cus;
+    if (n < 1) return false;
+    const int64_t b = (H + n - 1) / n;  // the largest band
     if (2 * (b + 2 * k) * wpr * 4 > 160 * 1024) return false;
     *nwg = (int)n;
     *B = (int)b;

@@ -28,7 +28,7 @@ struct StreamArgs {
 bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
-int64_t stream_strips(int64_t words, int ilv, int k);
+int64_t stream_strips(int64_t words, int ilv, int k, bool bounded);
 int stream_pair_split(int k, int ilv);
 int stream_wpb(int k, int ilv, bool bounded, bool wrap);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)

@@ -44,9 +44,12 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 // workgroups at 3 waves/SIMD (168 VGPRs; profiles/r1/w12_sweep*.log) in both torus variants.  The bounded
 // variant carries row/column masks and spills at that budget (profiles/r1/strip_bounded_sweep.log: bounded
 // K = 12 41k GCUPS with 12-wave workgroups, 74k with 8), so it keeps 8.
+#ifndef GOL_BOUNDED_W12
+#define GOL_BOUNDED_W12 0
+#endif
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
 struct Wpb {
-    static constexpr int value = (!BOUNDED && K == 12 && M == 2) ? 12 : kWavesPerBlock;
+    static constexpr int value = (GOL_BOUNDED_W12 || !BOUNDED) && K == 12 && M == 2 ? 12 : kWavesPerBlock;
 };
 
 // Block-edge words of the neighbouring lanes, by DPP (a half-rate VALU move on gfx950,
@@ -166,7 +169,16 @@ struct StreamWave {
     uint32_t colmask;  // bounded: ~0 for an on-board block
     int64_t row_bytes;
     int64_t seg_begin, seg_end, nsteps, ly0;
-    int64_t load_br;  // buffer row of the next level-0 row to load (uniform)
+    int64_t load_br;  // wrap: buffer row of the next level-0 row to load; else buffer row of step 0 (uniform)
+    int seglen = 0, step_lo = 0, step_hi = 0, mrow_lo = 0, mrow_hi = 0;
+    bool edge_fill = false;  // bounded: strips placed so that no lane is off the board (constructor)
+
+    // Bounded boards: trips [t_top, t_bot) produce no row off the board at any level (trip t produces the rows
+    // of steps t*R - K .. t*R + R - 2) and run the unmasked arithmetic of the torus strips; the others mask
+    // the rows off the board dead at every level.  A board narrower than a strip (no edge-fill strips) masks
+    // its columns in every trip: t_top = t_bot = 0.  Wave-uniform (the bounds are loop limits: a lane-varying
+    // exit would turn the trip loop into a divergent loop).
+    int t_top = 0, t_bot = 0;
 
     // level state: two row slots (X, Y) of block row sums (s, c) and the raw centre block of slot Y
     uint32_t sX[K][M], cX[K][M], sY[K][M], cY[K][M], aY[K][M];
@@ -201,8 +213,15 @@ struct StreamWave {
                                           int64_t sx, int64_t sy, int role = -1)
         : src(s), dst(d), a(args) {
         const int64_t nblocks = a.words / M;
+        // Bounded boards at least a strip wide (edge-fill strips): the first strip starts at the board's first
+        // block and the last ends at its last block, so the dead cells beyond the left / right edge arrive as
+        // the zeros the DPP moves write into lanes 0 / 63 (bound_ctrl), and no lane is ever off the board --
+        // no column mask at any level.  Interior strips overlap by two blocks as on a torus (halo lanes).
+        edge_fill = BOUNDED && !kNoHalo && nblocks >= kWave;
         // this lane's block column (may be off-board)
-        const int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
+        const int64_t cb = kNoHalo      ? sx * kWave + lane
+                           : edge_fill ? (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane
+                                        : sx * kInterior - 1 + lane;
         int64_t lc;
         if (BOUNDED) {
             const bool in = cb >= 0 && cb < nblocks;
@@ -228,6 +247,8 @@ struct StreamWave {
                 nl = floor_mod(nbc, nblocks);
             }
             nb_off = (int)((nl * M + nbw) * 4);
+        } else if (edge_fill) {  // lane 0 is a halo lane unless it is the board's first block, lane 63 unless the last
+            store_off = ((lane >= 1 || sx == 0) && (lane <= kInterior || sx == a.nstrips - 1)) ? load_off : kNoStore;
         } else {
             store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
         }
@@ -239,18 +260,42 @@ struct StreamWave {
             const int64_t b0 = seg_begin;
             seg_begin = b0 + group_cut(len, role);
             seg_end = b0 + group_cut(len, role + 1);
-            if (!WRAP_ROWS && !BOUNDED) {
+            if (!WRAP_ROWS) {
                 // the group cut is float VALU math: without this the segment bounds live in 8 VGPRs, and
                 // the ghost-row variant spills at the 3-waves/SIMD budget (a scratch reload every loop
-                // trip; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k GCUPS).  The single-board
-                // variant loses 4-8 % with it (its register allocation changes), so it keeps VGPR bounds.
+                // trip; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k GCUPS); on a bounded board the
+                // per-level row masks then stay scalar (s_cmp / s_cselect) instead of 64-bit VALU compares
+                // and v_cndmask.  The single-board torus variant loses 4-8 % with it (its register
+                // allocation changes), so it keeps VGPR bounds.
                 seg_begin = uniform64(seg_begin);
                 seg_end = uniform64(seg_end);
             }
         }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
+        seglen = (int)(seg_end - seg_begin);     // < 2^30 (plan_stream)
         ly0 = seg_begin - K;                     // level-0 row of step 0
         load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
+        if (BOUNDED) {  // steps whose row lies on the board: global row a.y0 + ly0 + st in [0, height)
+            const int64_t lo = -(a.y0 + ly0), hi = a.height - (a.y0 + ly0);
+            const int64_t cap = (int64_t)1 << 30;
+            mrow_lo = (int)(lo < -cap ? -cap : (lo > cap ? cap : lo));
+            mrow_hi = (int)(hi < -cap ? -cap : (hi > cap ? cap : hi));
+        }
+        if (BOUNDED && edge_fill) {
+            // first trip whose lowest produced row is on the board: t*R - K >= mrow_lo; first trip whose
+            // highest is off it: t*R + R - 2 >= mrow_hi
+            const int up = mrow_lo + K, dn = mrow_hi - R + 2;
+            t_top = up <= 0 ? 0 : (up + R - 1) / R;
+            t_bot = dn <= 0 ? 0 : (dn + R - 1) / R;
+        }
+        if (!WRAP_ROWS) {
+            // steps whose level-0 row lies in the buffer, as 32-bit step indices: the per-row clamp below is
+            // then 32-bit scalar arithmetic (the scalar unit has no 64-bit ordered compare)
+            const int64_t lo = -load_br, hi = a.rows + 2 * a.ghost - 1 - load_br;
+            const int64_t cap = (int64_t)1 << 30;
+            step_lo = (int)(lo < -cap ? -cap : (lo > cap ? cap : lo));
+            step_hi = (int)(hi < -cap ? -cap : (hi > cap ? cap : hi));
+        }
 #pragma unroll
         for (int g = 0; g < K; g++)
 #pragma unroll
@@ -260,33 +305,39 @@ struct StreamWave {
     // Load the next R level-0 rows.  Loads are unconditional (addresses clamped, values masked) so every
     // trip issues a fixed number of memory operations and the compiler waits for exactly the loads.
     __device__ __forceinline__ void load(uint32_t (&buf)[R][M], uint32_t (&nb)[R], int64_t first_step) {
-        const int64_t buf_rows = a.rows + 2 * a.ghost;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             int64_t br = load_br;
             if (WRAP_ROWS) {
                 load_br = br + 1 == a.rows ? 0 : br + 1;
             } else {
-                load_br = br + 1;
                 // rows outside the buffer (beyond a bounded board's edge, or past the segment's last
                 // step) are never used unmasked: clamp the address into the buffer
-                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+                int st = (int)first_step + r;
+                st = st < step_lo ? step_lo : (st > step_hi ? step_hi : st);
+                br = load_br + st;
             }
             V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
             if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
             if (BOUNDED) {
-                const int64_t gy = a.y0 + ly0 + first_step + r;
-                const bool row_in = gy >= 0 && gy < a.height;
-                const uint32_t m = row_in ? colmask : 0u;
+                const uint32_t rm = row_mask((int)first_step + r);
 #pragma unroll
-                for (int j = 0; j < M; j++) buf[r][j] &= m;
-                if (kNoHalo) nb[r] &= row_in ? nbmask : 0u;
+                for (int j = 0; j < M; j++) buf[r][j] = lut3<0x80>(buf[r][j], colmask, rm);  // a & b & c
+                if (kNoHalo) nb[r] = lut3<0x80>(nb[r], nbmask, rm);
             }
         }
     }
 
+    // Bounded boards: all-ones if the row of step `st` (level-0 row ly0 + st, or at level g the row it produces)
+    // is on the board, else 0.  32-bit step bounds set up once (the scalar unit has no 64-bit ordered compare;
+    // a 64-bit one goes to the VALU as v_cmp_*_u64 + v_cndmask per row and level), wave-uniform.
+    __device__ __forceinline__ uint32_t row_mask(int st) const {
+        return (st >= mrow_lo && st < mrow_hi) ? 0xffffffffu : 0u;
+    }
+
     // One level, one row: window (prev P, centre C) + new row v -> next generation of the C row.
     // The new row's sums overwrite the P slot (it becomes the centre slot of the following row).
+    template <bool MASK>
     __device__ __forceinline__ void level_row(uint32_t (&v)[M], uint32_t left, uint32_t right, uint32_t (&sP)[M],
                                               uint32_t (&cP)[M],
                                               const uint32_t (&sC)[M], const uint32_t (&cC)[M],
@@ -296,7 +347,7 @@ struct StreamWave {
 #pragma unroll
         for (int j = 0; j < M; j++) {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
-            if (BOUNDED) out[j] &= rowmask;
+            if (BOUNDED && MASK) out[j] = lut3<0x80>(out[j], colmask, rowmask);  // dead off the board
             sP[j] = sN[j];
             cP[j] = cN[j];
         }
@@ -304,17 +355,15 @@ struct StreamWave {
 
     // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
-    template <bool SKIP>
+    template <bool SKIP, bool MASK>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
-        const int64_t lyt = ly0 + t * R;
         if constexpr (kNoHalo) {  // K = 1: lanes 0 / 63 keep the loaded neighbour word (bound_ctrl off)
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
-                if (BOUNDED) {
-                    const int64_t gy = a.y0 + lyt + r - 1;
-                    m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
-                    m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
+                if (BOUNDED && MASK) {
+                    m0 = row_mask((int)t * R + r - 1);
+                    m1 = row_mask((int)t * R + r);
                 }
                 const uint32_t l0 = (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r], (int)v[r][M - 1], 0x138, 0xf, 0xf, false);
                 const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r], (int)v[r][0], 0x130, 0xf, 0xf, false);
@@ -323,8 +372,8 @@ struct StreamWave {
                 const uint32_t r1 =
                     (uint32_t)__builtin_amdgcn_update_dpp((int)nb[r + 1], (int)v[r + 1][0], 0x130, 0xf, 0xf, false);
                 uint32_t o0[M], o1[M];
-                level_row(v[r], l0, r0, sX[0], cX[0], sY[0], cY[0], aY[0], m0, o0);
-                level_row(v[r + 1], l1, r1, sY[0], cY[0], sX[0], cX[0], v[r], m1, o1);
+                level_row<MASK>(v[r], l0, r0, sX[0], cX[0], sY[0], cY[0], aY[0], m0, o0);
+                level_row<MASK>(v[r + 1], l1, r1, sY[0], cY[0], sX[0], cX[0], v[r], m1, o1);
 #pragma unroll
                 for (int j = 0; j < M; j++) {
                     aY[0][j] = v[r + 1][j];
@@ -347,15 +396,14 @@ struct StreamWave {
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
-                if (BOUNDED) {  // cells outside the board stay dead at every generation (Script.fsx:11)
-                    const int64_t gy = a.y0 + lyt + r - g - 1;  // row produced from v[r] at level g + 1
-                    m0 = (gy >= 0 && gy < a.height) ? colmask : 0u;
-                    m1 = (gy + 1 >= 0 && gy + 1 < a.height) ? colmask : 0u;
+                if (BOUNDED && MASK) {  // cells outside the board stay dead at every generation (Script.fsx:11)
+                    m0 = row_mask((int)t * R + r - g - 1);  // row produced from v[r] at level g + 1
+                    m1 = row_mask((int)t * R + r - g);
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-                level_row(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-                level_row(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
+                level_row<MASK>(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row<MASK>(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
                           o1);
 #pragma unroll
                 for (int j = 0; j < M; j++) {
@@ -380,11 +428,11 @@ struct StreamWave {
     // descriptor (num_records 0): the stores are dropped by the range check with no branch, and the row
     // address is clamped so no out-of-buffer pointer is ever formed.
     __device__ __forceinline__ void store_masked(const uint32_t (&v)[R][M], int64_t t) {
-        const int64_t lo = ly0 + t * R - K;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const bool valid = lo + r >= seg_begin && lo + r < seg_end;
-            store_row(v[r], valid ? lo + r : seg_begin, valid);
+            const int d = (int)t * R + r - 2 * K;  // output row (ly0 + t*R + r - K) - seg_begin
+            const bool valid = d >= 0 && d < seglen;
+            store_row(v[r], seg_begin + (valid ? d : 0), valid);
         }
     }
 };
@@ -446,27 +494,46 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     }
     w.load(A, NA, 0);
     auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
-                    int64_t tt, auto skip) {
+                    int64_t tt, auto skip, auto mask) {
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(other, tt - 1);
         w.load(other, nother, (tt + 1) * R);
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
-        w.template process<decltype(skip)::value>(cur, ncur, tt);
+        w.template process<decltype(skip)::value, decltype(mask)::value>(cur, ncur, tt);
     };
     using Skip = std::true_type;
     using NoSkip = std::false_type;
+    using Mask = std::true_type;
+    using NoMask = std::false_type;
     const int64_t fill_pairs = (t_fill < ntrips ? t_fill : ntrips) / 2;
     int64_t t = 0;
     for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
-        trip(A, B, NA, NB, t, Skip{});
-        trip(B, A, NB, NA, t + 1, Skip{});
+        // (bounded: masked, the few fill trips of a segment at the top edge produce rows above the board)
+        trip(A, B, NA, NB, t, Skip{}, std::integral_constant<bool, BOUNDED>{});
+        trip(B, A, NB, NA, t + 1, Skip{}, std::integral_constant<bool, BOUNDED>{});
     }
-    for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
-        trip(A, B, NA, NB, t, NoSkip{});
-        trip(B, A, NB, NA, t + 1, NoSkip{});
+    // steady state (the odd fill / transition trip runs here unskipped); on a bounded board the trips that
+    // produce rows off the board (near its top and bottom edges) run masked
+    int64_t t_end = ntrips;
+    if constexpr (BOUNDED) {
+        for (; t + 1 < ntrips && t < w.t_top; t += 2) {
+            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
+            trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
+        }
+        t_end = w.t_bot < ntrips ? w.t_bot : ntrips;
+    }
+    for (; t + 1 < t_end; t += 2) {
+        trip(A, B, NA, NB, t, NoSkip{}, NoMask{});
+        trip(B, A, NB, NA, t + 1, NoSkip{}, NoMask{});
+    }
+    if constexpr (BOUNDED) {
+        for (; t + 1 < ntrips; t += 2) {
+            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
+            trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
+        }
     }
     if (t < ntrips) {  // odd trip count: one more trip, outputs land in A
-        trip(A, B, NA, NB, t, NoSkip{});
+        trip(A, B, NA, NB, t, NoSkip{}, std::integral_constant<bool, BOUNDED>{});
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
         w.store_masked(A, t);
     } else {
@@ -523,9 +590,13 @@ static const void* kernel_for(int k, int ilv, bool bounded, bool wrap) {
     return nullptr;
 }
 
-int64_t stream_strips(int64_t words, int ilv, int k) {
-    const int per = k == 1 ? kWave : kInterior;  // K = 1: halo-free strips
-    return (words / ilv + per - 1) / per;
+int64_t stream_strips(int64_t words, int ilv, int k, bool bounded) {
+    const int64_t nblocks = words / ilv;
+    if (k == 1) return (nblocks + kWave - 1) / kWave;  // K = 1: halo-free strips
+    // bounded edge-fill strips (StreamWave::edge_fill): strip 0 stores blocks [0, 63), strip s stores
+    // [62 s + 1, 62 s + 63), the last ends at the board's last block
+    if (bounded && nblocks >= kWave) return (nblocks - 1 + kInterior - 1) / kInterior;
+    return (nblocks + kInterior - 1) / kInterior;
 }
 
 // Waves per workgroup of a variant (Wpb)
@@ -595,7 +666,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         return e ? std::atoll(e) : 0LL;
     }();
     a.split = stream_pair_split(k, a.ilv);
-    a.nstrips = stream_strips(a.words, a.ilv, k);
+    a.nstrips = stream_strips(a.words, a.ilv, k, bounded);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
         a.nsegs = 0;
@@ -624,6 +695,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         if (nsegs > max_segs) nsegs = max_segs;
         seg = (rows + nsegs - 1) / nsegs;
     }
+    if (seg > ((int64_t)1 << 30)) seg = (int64_t)1 << 30;  // the kernel counts a segment's rows in 32 bits
     a.seg = seg;
     a.nsegs = (rows + seg - 1) / seg;
 }

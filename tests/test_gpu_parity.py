@@ -384,3 +384,21 @@ def test_native_host_mirror_driver():
     out = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stdout + out.stderr
     assert '"failures": []' in out.stdout
+
+
+# ---------------------------------------------------------------- bounded boards: edge-fill strips
+@pytest.mark.parametrize("ilv", [1, 2])
+@pytest.mark.parametrize("nblocks", [64, 65, 124, 125, 126, 127, 189, 1024])
+def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks):
+    """Bounded boards at least a strip (64 blocks) wide place their first strip at the board's left edge and
+    the last at its right edge (the dead cells beyond the edges arrive as the DPP moves' zero fill), and run
+    only the trips that produce rows off the board masked (Script.fsx:6-13).  Every strip-count boundary
+    (nblocks around multiples of 62), the top/bottom trips of the first/last segments, a deep block and a
+    remainder pass, against the oracle."""
+    w = 32 * ilv * nblocks
+    h = 300 if nblocks < 1024 else 64
+    b0 = _rand(h, w, nblocks * 10 + ilv, p=0.4)
+    for k in (16, 12, 8):
+        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv) as b:
+            b.set_cells(b0).step(2 * k + 5)
+            np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 2 * k + 5, 1), err_msg=f"k={k}")

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Repeated, interleaved A/B of library variants on the 65536^2 board (ABAB order averages drift).
-#   tools/ab_rep.sh out.log reps "ilv:ks ilv:ks ..." lib1.so lib2.so ...
+#   [AB_BOUNDARY=1] tools/ab_rep.sh out.log reps "ilv:ks ilv:ks ..." lib1.so lib2.so ...
 out=$1; reps=$2; cfgs=$3; shift 3
 : > $out
 for rep in $(seq $reps); do
@@ -8,7 +8,7 @@ for rep in $(seq $reps); do
     for cfg in $cfgs; do
       ilv=${cfg%%:*}; ks=${cfg#*:}
       echo "rep=$rep lib=$(basename $L) ilv=$ilv" >> $out
-      GOL_LIB=$PWD/$L GOL_ILV=$ilv timeout -k 10 120 python tools/sweep.py --ks $ks --passes 16 2>/dev/null | grep '^{' >> $out || exit 1
+      GOL_LIB=$PWD/$L GOL_ILV=$ilv timeout -k 10 120 python tools/sweep.py --ks $ks --passes 16 --boundary ${AB_BOUNDARY:-0} 2>/dev/null | grep '^{' >> $out || exit 1
     done
   done
 done
