@@ -217,11 +217,12 @@ struct StreamWave {
         // block and the last ends at its last block, so the dead cells beyond the left / right edge arrive as
         // the zeros the DPP moves write into lanes 0 / 63 (bound_ctrl), and no lane is ever off the board --
         // no column mask at any level.  Interior strips overlap by two blocks as on a torus (halo lanes).
-        edge_fill = BOUNDED && !kNoHalo && nblocks >= kWave;
         // this lane's block column (may be off-board)
-        const int64_t cb = kNoHalo      ? sx * kWave + lane
-                           : edge_fill ? (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane
-                                        : sx * kInterior - 1 + lane;
+        int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
+        if constexpr (BOUNDED && !kNoHalo) {
+            edge_fill = nblocks >= kWave;
+            if (edge_fill) cb = (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane;
+        }
         int64_t lc;
         if (BOUNDED) {
             const bool in = cb >= 0 && cb < nblocks;
@@ -247,7 +248,7 @@ struct StreamWave {
                 nl = floor_mod(nbc, nblocks);
             }
             nb_off = (int)((nl * M + nbw) * 4);
-        } else if (edge_fill) {  // lane 0 is a halo lane unless it is the board's first block, lane 63 unless the last
+        } else if (BOUNDED && edge_fill) {  // lane 0 is a halo lane unless it is the board's first block, lane 63 unless the last
             store_off = ((lane >= 1 || sx == 0) && (lane <= kInterior || sx == a.nstrips - 1)) ? load_off : kNoStore;
         } else {
             store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
@@ -272,7 +273,7 @@ struct StreamWave {
             }
         }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
-        seglen = (int)(seg_end - seg_begin);     // < 2^30 (plan_stream)
+        if (BOUNDED) seglen = (int)(seg_end - seg_begin);  // < 2^30 (plan_stream)
         ly0 = seg_begin - K;                     // level-0 row of step 0
         load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
         if (BOUNDED) {  // steps whose row lies on the board: global row a.y0 + ly0 + st in [0, height)
@@ -288,7 +289,7 @@ struct StreamWave {
             t_top = up <= 0 ? 0 : (up + R - 1) / R;
             t_bot = dn <= 0 ? 0 : (dn + R - 1) / R;
         }
-        if (!WRAP_ROWS) {
+        if (BOUNDED) {
             // steps whose level-0 row lies in the buffer, as 32-bit step indices: the per-row clamp below is
             // then 32-bit scalar arithmetic (the scalar unit has no 64-bit ordered compare)
             const int64_t lo = -load_br, hi = a.rows + 2 * a.ghost - 1 - load_br;
@@ -310,12 +311,18 @@ struct StreamWave {
             int64_t br = load_br;
             if (WRAP_ROWS) {
                 load_br = br + 1 == a.rows ? 0 : br + 1;
-            } else {
+            } else if (BOUNDED) {
                 // rows outside the buffer (beyond a bounded board's edge, or past the segment's last
-                // step) are never used unmasked: clamp the address into the buffer
+                // step) are never used unmasked: clamp the address into the buffer (32-bit step indices,
+                // scalar; load_br stays the buffer row of step 0)
                 int st = (int)first_step + r;
                 st = st < step_lo ? step_lo : (st > step_hi ? step_hi : st);
                 br = load_br + st;
+            } else {
+                // ghost-row strips: the same clamp on 64-bit rows (this variant's measured instruction stream)
+                const int64_t buf_rows = a.rows + 2 * a.ghost;
+                load_br = br + 1;
+                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
             V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
             if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
@@ -357,6 +364,7 @@ struct StreamWave {
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
     template <bool SKIP, bool MASK>
     __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
+        [[maybe_unused]] const int64_t lyt = ly0 + t * R;
         if constexpr (kNoHalo) {  // K = 1: lanes 0 / 63 keep the loaded neighbour word (bound_ctrl off)
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
@@ -428,11 +436,20 @@ struct StreamWave {
     // descriptor (num_records 0): the stores are dropped by the range check with no branch, and the row
     // address is clamped so no out-of-buffer pointer is ever formed.
     __device__ __forceinline__ void store_masked(const uint32_t (&v)[R][M], int64_t t) {
+        if constexpr (BOUNDED) {  // 32-bit step arithmetic: scalar compares
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int d = (int)t * R + r - 2 * K;  // output row (ly0 + t*R + r - K) - seg_begin
-            const bool valid = d >= 0 && d < seglen;
-            store_row(v[r], seg_begin + (valid ? d : 0), valid);
+            for (int r = 0; r < R; r++) {
+                const int d = (int)t * R + r - 2 * K;  // output row (ly0 + t*R + r - K) - seg_begin
+                const bool valid = d >= 0 && d < seglen;
+                store_row(v[r], seg_begin + (valid ? d : 0), valid);
+            }
+        } else {  // the torus variants keep their measured instruction streams (profiles/r2/ab_torus_d.log)
+            const int64_t lo = ly0 + t * R - K;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const bool valid = lo + r >= seg_begin && lo + r < seg_end;
+                store_row(v[r], valid ? lo + r : seg_begin, valid);
+            }
         }
     }
 };
@@ -493,52 +510,74 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         for (int j = 0; j < M; j++) B[r][j] = 0;
     }
     w.load(A, NA, 0);
-    auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
-                    int64_t tt, auto skip, auto mask) {
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        w.store_masked(other, tt - 1);
-        w.load(other, nother, (tt + 1) * R);
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
-        w.template process<decltype(skip)::value, decltype(mask)::value>(cur, ncur, tt);
-    };
     using Skip = std::true_type;
     using NoSkip = std::false_type;
-    using Mask = std::true_type;
-    using NoMask = std::false_type;
     const int64_t fill_pairs = (t_fill < ntrips ? t_fill : ntrips) / 2;
     int64_t t = 0;
-    for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
-        // (bounded: masked, the few fill trips of a segment at the top edge produce rows above the board)
-        trip(A, B, NA, NB, t, Skip{}, std::integral_constant<bool, BOUNDED>{});
-        trip(B, A, NB, NA, t + 1, Skip{}, std::integral_constant<bool, BOUNDED>{});
-    }
-    // steady state (the odd fill / transition trip runs here unskipped); on a bounded board the trips that
-    // produce rows off the board (near its top and bottom edges) run masked
-    int64_t t_end = ntrips;
-    if constexpr (BOUNDED) {
+    if constexpr (!BOUNDED) {
+        auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
+                        int64_t tt, auto skip) {
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(other, tt - 1);
+            w.load(other, nother, (tt + 1) * R);
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
+            w.template process<decltype(skip)::value, false>(cur, ncur, tt);
+        };
+        for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
+            trip(A, B, NA, NB, t, Skip{});
+            trip(B, A, NB, NA, t + 1, Skip{});
+        }
+        for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
+            trip(A, B, NA, NB, t, NoSkip{});
+            trip(B, A, NB, NA, t + 1, NoSkip{});
+        }
+        if (t < ntrips) {  // odd trip count: one more trip, outputs land in A
+            trip(A, B, NA, NB, t, NoSkip{});
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(A, t);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(B, t - 1);
+        }
+    } else {
+        // Bounded board: the trips that produce rows off the board (the fill trips and, in the steady state,
+        // t < t_top or t >= t_bot: near the board's top and bottom edges) mask them dead at every level; the
+        // others run the unmasked arithmetic of the torus strips.
+        auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
+                        int64_t tt, auto skip, auto mask) {
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(other, tt - 1);
+            w.load(other, nother, (tt + 1) * R);
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
+            w.template process<decltype(skip)::value, decltype(mask)::value>(cur, ncur, tt);
+        };
+        using Mask = std::true_type;
+        using NoMask = std::false_type;
+        for (int64_t p = 0; p < fill_pairs; p++, t += 2) {
+            trip(A, B, NA, NB, t, Skip{}, Mask{});
+            trip(B, A, NB, NA, t + 1, Skip{}, Mask{});
+        }
         for (; t + 1 < ntrips && t < w.t_top; t += 2) {
             trip(A, B, NA, NB, t, NoSkip{}, Mask{});
             trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
         }
-        t_end = w.t_bot < ntrips ? w.t_bot : ntrips;
-    }
-    for (; t + 1 < t_end; t += 2) {
-        trip(A, B, NA, NB, t, NoSkip{}, NoMask{});
-        trip(B, A, NB, NA, t + 1, NoSkip{}, NoMask{});
-    }
-    if constexpr (BOUNDED) {
+        const int64_t t_end = w.t_bot < ntrips ? w.t_bot : ntrips;
+        for (; t + 1 < t_end; t += 2) {
+            trip(A, B, NA, NB, t, NoSkip{}, NoMask{});
+            trip(B, A, NB, NA, t + 1, NoSkip{}, NoMask{});
+        }
         for (; t + 1 < ntrips; t += 2) {
             trip(A, B, NA, NB, t, NoSkip{}, Mask{});
             trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
         }
-    }
-    if (t < ntrips) {  // odd trip count: one more trip, outputs land in A
-        trip(A, B, NA, NB, t, NoSkip{}, std::integral_constant<bool, BOUNDED>{});
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        w.store_masked(A, t);
-    } else {
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        w.store_masked(B, t - 1);
+        if (t < ntrips) {
+            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(A, t);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(B, t - 1);
+        }
     }
 #if GOL_STAMP
     __builtin_amdgcn_s_waitcnt(0);
