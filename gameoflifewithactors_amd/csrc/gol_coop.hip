@@ -12,11 +12,13 @@
 // and before the next block waits only for its two neighbour bands (their halo rows, and that they have
 // finished reading the rows it is about to overwrite).  No grid barrier, one launch per call.
 //
-// Hand-off protocol (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility"): every wave's
-// stores drain (s_waitcnt vmcnt(0)), workgroup barrier, one lane: agent-scope release fence, s_waitcnt
-// vmcnt(0) (the compiler may drop the one after the fence), relaxed agent-scope store of the flag; the
-// consumer polls with relaxed agent-scope loads + s_sleep, then an agent-scope acquire fence and a workgroup
-// barrier before its plain loads.  Residency: the grid is one workgroup per CU, each asking for more than
+// The band stays in LDS for the whole call; only its first and last k rows are handed to the neighbours per
+// block.  Hand-off protocol (MI355X_MICROARCH.md "Valid forms", first row of the sc1 table: hipMalloc, one
+// workgroup per CU): the edge rows are stored write-through (sc1), every storing wave drains them
+// (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the band's flag (sc1); the consumer's one
+// lane polls the flags with sc1 loads, a workgroup barrier, and every wave loads the rows with sc1 loads --
+// no release / acquire fences (they write back / invalidate whole caches: MI355X_MICROARCH.md
+// "publish-large").  Residency: the grid is one workgroup per CU, each asking for more than
 // half of the CU's LDS, launched cooperatively (the runtime rejects a grid that cannot be co-resident); every
 // spin is bounded and a timed-out wait raises an error word the host checks on the next synchronisation.
 #include "gol_internal.h"
@@ -63,6 +65,14 @@ __device__ __forceinline__ bool wait_flag(const unsigned* f, unsigned target) {
     return false;
 }
 
+// sc1 (write-through / L2-coherent) word store and load for the handed-off edge rows
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool BOUNDED>
 __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
     extern __shared__ uint32_t lds[];
@@ -73,49 +83,59 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
     const int y1 = (int)((int64_t)a.H * (band + 1) / a.nwg);
     const int own = y1 - y0;
     const int wpr = a.wpr;
-    const int stride = (a.B + 2 * a.K) * wpr;  // words per LDS buffer
+    const int K = a.K;
+    const int stride = (a.B + 2 * K) * wpr;  // words per LDS buffer; local row K + i = global row y0 + i
     // neighbour bands (a bounded board's end bands have one; a one-band torus is its own neighbour)
     const int up = band > 0 ? band - 1 : (BOUNDED ? -1 : a.nwg - 1);
     const int dn = band + 1 < a.nwg ? band + 1 : (BOUNDED ? -1 : 0);
-    // column-segment items: `segs` row segments per column
-    const int segs = wpr >= kThreads ? 1 : kThreads / wpr;
+    const int segs = wpr >= kThreads ? 1 : kThreads / wpr;  // row segments per column
     const int items = wpr * segs;
-    int cur = a.cur;
-    const int nblk = (a.gens + a.K - 1) / a.K;
+    const int nblk = (a.gens + K - 1) / K;
+    auto wrap = [&](int gy) { return gy < 0 ? gy + a.H : (gy >= a.H ? gy - a.H : gy); };
+    auto on_board = [&](int gy) { return gy >= 0 && gy < a.H; };
+    uint32_t* A = lds;  // the band (+ halo) at the start of a block
+    uint32_t* Bf = lds + stride;
+    // the band and K halo rows per side, once, from the board
+    {
+        const uint32_t* src = a.buf[a.cur];
+        const int n = own + 2 * K;
+        for (int i = tid; i < n * wpr; i += kThreads) {
+            const int r = i / wpr, c = i - r * wpr;
+            const int gy = y0 - K + r;
+            uint32_t v = 0;
+            if (on_board(gy) || !BOUNDED) v = src[(int64_t)wrap(gy) * a.pitch + c];
+            A[r * wpr + c] = v;
+        }
+        __syncthreads();
+    }
+    int x = a.cur;  // board buffer the latest hand-off went to
     for (int blk = 0; blk < nblk; blk++) {
-        const int k = a.gens - blk * a.K < a.K ? a.gens - blk * a.K : a.K;
-        if (blk > 0) {  // the neighbours finished block blk - 1: their band rows are stored, our rows are read
+        const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
+        if (blk > 0) {
+            // the neighbours finished block blk - 1: their edge rows are in buf[x] (write-through), and
+            // they have read ours from the buffer we are about to write (blk + 1 alternates)
             if (tid == 0) {
                 bool ok = true;
                 if (up >= 0) ok = wait_flag(a.flags + up, (unsigned)blk) && ok;
                 if (dn >= 0) ok = wait_flag(a.flags + dn, (unsigned)blk) && ok;
                 if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            // halo rows: k above (the up band's last rows), k below (the down band's first rows)
+            const uint32_t* src = a.buf[x];
+            for (int i = tid; i < 2 * k * wpr; i += kThreads) {
+                const int r = i / wpr, c = i - r * wpr;
+                const int lr = r < k ? K - k + r : K + own + (r - k);  // local row
+                const int gy = y0 - K + lr;
+                uint32_t v = 0;
+                if (on_board(gy) || !BOUNDED) v = ld_sc1(src + (int64_t)wrap(gy) * a.pitch + c);
+                A[lr * wpr + c] = v;
             }
             __syncthreads();
         }
-        // 1. band + k halo rows -> LDS buffer 0 (local row i = global row y0 - k + i)
-        const int n = own + 2 * k;
-        const uint32_t* src = a.buf[cur];
-        for (int i = tid; i < n * wpr; i += kThreads) {
-            const int r = i / wpr, c = i - r * wpr;
-            int gy = y0 - k + r;
-            uint32_t v = 0;
-            if (gy >= 0 && gy < a.H) {
-                v = src[(int64_t)gy * a.pitch + c];
-            } else if (!BOUNDED) {
-                gy = gy < 0 ? gy + a.H : gy - a.H;
-                v = src[(int64_t)gy * a.pitch + c];
-            }
-            lds[r * wpr + c] = v;
-        }
-        __syncthreads();
-        // 2. k generations in LDS: generation j writes local rows [j + 1, n - 1 - j)
-        uint32_t* A = lds;
-        uint32_t* Bf = lds + stride;
+        // k generations in LDS: generation j writes local rows [K - k + 1 + j, K + own + k - 1 - j)
         for (int j = 0; j < k; j++) {
-            const int r0 = j + 1, r1 = n - 1 - j, rows = r1 - r0;
+            const int r0 = K - k + 1 + j, rows = own + 2 * (k - 1 - j);
             for (int it = tid; it < items; it += kThreads) {
                 const int sg = it / wpr, c = it - sg * wpr;
                 const int ra = r0 + sg * rows / segs, rb = r0 + (sg + 1) * rows / segs;
@@ -126,10 +146,7 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
                 for (int r = ra; r < rb; r++) {
                     const uint32_t mN = lds_row<BOUNDED>(A + (r + 1) * wpr, wpr, c, sN, cN);
                     uint32_t v = life_next(sP, cP, sC, cC, sN, cN, mC);
-                    if (BOUNDED) {
-                        const int gy = y0 - k + r;
-                        if (gy < 0 || gy >= a.H) v = 0u;  // dead outside the board at every generation
-                    }
+                    if (BOUNDED && !on_board(y0 - K + r)) v = 0u;  // dead outside the board at every generation
                     Bf[r * wpr + c] = v;
                     sP = sC, cP = cC, sC = sN, cC = cN, mC = mN;
                 }
@@ -139,20 +156,24 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
             A = Bf;
             Bf = t;
         }
-        // 3. the band (local rows [k, k + own)) -> the other buffer, then publish
-        uint32_t* dst = a.buf[cur ^ 1];
-        for (int i = tid; i < own * wpr; i += kThreads) {
+        if (blk + 1 == nblk) break;
+        // hand-off: the band's first and last k rows, write-through, to the other board buffer
+        x ^= 1;
+        uint32_t* dst = a.buf[x];
+        for (int i = tid; i < 2 * k * wpr; i += kThreads) {
             const int r = i / wpr, c = i - r * wpr;
-            dst[(int64_t)(y0 + r) * a.pitch + c] = A[(k + r) * wpr + c];
+            const int lr = r < k ? K + r : K + own - k + (r - k);
+            st_sc1(dst + (int64_t)(y0 - K + lr) * a.pitch + c, A[lr * wpr + c]);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        cur ^= 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores complete ...
+        __syncthreads();                                   // ... before one lane publishes for all
+        if (tid == 0) __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the whole band to the result buffer (the host flips the board buffer once per block)
+    uint32_t* dst = a.buf[a.cur ^ (nblk & 1)];
+    for (int i = tid; i < own * wpr; i += kThreads) {
+        const int r = i / wpr, c = i - r * wpr;
+        dst[(int64_t)(y0 + r) * a.pitch + c] = A[(K + r) * wpr + c];
     }
 }
 

@@ -59,24 +59,36 @@ __global__ __launch_bounds__(64) void gol_wave_resident(const void* __restrict__
     const uint32_t lastmask = lb == 31 ? 0xffffffffu : (lbbit << 1) - 1u;
     uint32_t w[RPL][NW];
 
-    // ---- load this lane's rows
+    // ---- load the board: byte boards row by row, 64 cells per wave-wide coalesced load, packed by ballot (the
+    // 64-bit lane mask is the next two words of the row) into the lane that owns the row; packed boards one word
+    // load per owned word
 #pragma unroll
-    for (int i = 0; i < RPL; i++) {
-        const int y = lane * RPL + i;
+    for (int i = 0; i < RPL; i++)
 #pragma unroll
-        for (int j = 0; j < NW; j++) {
-            uint32_t v = 0;
-            if (active) {
-                if (BYTES) {
-                    const uint8_t* row = static_cast<const uint8_t*>(src) + (int64_t)y * W;
-                    const int x0 = 32 * j, n = W - x0 < 32 ? W - x0 : 32;
-                    for (int b = 0; b < n; b++) v |= (row[x0 + b] != 0 ? 1u : 0u) << b;
-                } else {
-                    v = static_cast<const uint32_t*>(src)[(int64_t)y * pitch + j];
+        for (int j = 0; j < NW; j++) w[i][j] = 0;
+    if (BYTES) {
+        const uint8_t* cells = static_cast<const uint8_t*>(src);
+        for (int L = 0; L < nl; L++) {
+#pragma unroll
+            for (int i = 0; i < RPL; i++) {
+                const uint8_t* row = cells + (int64_t)(L * RPL + i) * W;
+#pragma unroll
+                for (int c = 0; c < (NW + 1) / 2; c++) {
+                    const int x = 64 * c + lane;
+                    const uint64_t m = __ballot(x < W && row[x] != 0);
+                    if (lane == L) {
+                        w[i][2 * c] = (uint32_t)m;
+                        if (2 * c + 1 < NW) w[i][2 * c + 1] = (uint32_t)(m >> 32);
+                    }
                 }
             }
-            w[i][j] = v;
         }
+    } else if (active) {
+#pragma unroll
+        for (int i = 0; i < RPL; i++)
+#pragma unroll
+            for (int j = 0; j < NW; j++)
+                w[i][j] = static_cast<const uint32_t*>(src)[(int64_t)(lane * RPL + i) * pitch + j];
     }
     // lanes the rows above the first row / below the last row come from (ds_bpermute byte addresses)
     const int up_lane = lane == 0 ? nl - 1 : lane - 1;
@@ -109,22 +121,32 @@ __global__ __launch_bounds__(64) void gol_wave_resident(const void* __restrict__
             }
     }
 
-    // ---- store
-    if (!active) return;
+    // ---- store: byte boards row by row, each lane writing one cell of a 64-cell run (the owner lane's two
+    // words read as scalars), packed boards one word store per owned word
+    if (BYTES) {
+        uint8_t* cells = static_cast<uint8_t*>(dst);
+        for (int L = 0; L < nl; L++) {
 #pragma unroll
-    for (int i = 0; i < RPL; i++) {
-        const int y = lane * RPL + i;
+            for (int i = 0; i < RPL; i++) {
+                uint8_t* row = cells + (int64_t)(L * RPL + i) * W;
 #pragma unroll
-        for (int j = 0; j < NW; j++) {
-            if (BYTES) {
-                uint8_t* row = static_cast<uint8_t*>(dst) + (int64_t)y * W;
-                const int x0 = 32 * j, n = W - x0 < 32 ? W - x0 : 32;
-                for (int b = 0; b < n; b++) row[x0 + b] = (uint8_t)((w[i][j] >> b) & 1u);
-            } else {
-                static_cast<uint32_t*>(dst)[(int64_t)y * pitch + j] = w[i][j];
+                for (int c = 0; c < (NW + 1) / 2; c++) {
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)w[i][2 * c], L);
+                    const uint32_t hi =
+                        2 * c + 1 < NW ? (uint32_t)__builtin_amdgcn_readlane((int)w[i][2 * c + 1], L) : 0u;
+                    const int x = 64 * c + lane;
+                    const uint32_t word = lane < 32 ? lo : hi;
+                    if (x < W) row[x] = (uint8_t)((word >> (lane & 31)) & 1u);
+                }
             }
         }
+        return;
     }
+    if (!active) return;
+#pragma unroll
+    for (int i = 0; i < RPL; i++)
+#pragma unroll
+        for (int j = 0; j < NW; j++) static_cast<uint32_t*>(dst)[(int64_t)(lane * RPL + i) * pitch + j] = w[i][j];
 }
 
 template <int NW, int RPL>
