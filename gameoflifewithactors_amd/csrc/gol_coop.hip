@@ -90,6 +90,7 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
     const int dn = band + 1 < a.nwg ? band + 1 : (BOUNDED ? -1 : 0);
     const int segs = wpr >= kThreads ? 1 : kThreads / wpr;  // row segments per column
     const int items = wpr * segs;
+    const int my_sg = tid / wpr, my_c = tid - my_sg * wpr;  // this thread's first item
     const int nblk = (a.gens + K - 1) / K;
     auto wrap = [&](int gy) { return gy < 0 ? gy + a.H : (gy >= a.H ? gy - a.H : gy); };
     auto on_board = [&](int gy) { return gy >= 0 && gy < a.H; };
@@ -133,12 +134,23 @@ __global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
             }
             __syncthreads();
         }
-        // k generations in LDS: generation j writes local rows [K - k + 1 + j, K + own + k - 1 - j)
+        // k generations in LDS: generation j writes local rows [K - k + 1 + j, K + own + k - 1 - j).  Each
+        // item's row segment is fixed for the block (split of generation 0's rows) and clipped per generation:
+        // no division in the generation loop.
+        const int g0 = K - k + 1, g1 = K + own + k - 1;
+        const int my_ra = g0 + my_sg * (g1 - g0) / segs, my_rb = g0 + (my_sg + 1) * (g1 - g0) / segs;
         for (int j = 0; j < k; j++) {
-            const int r0 = K - k + 1 + j, rows = own + 2 * (k - 1 - j);
+            const int r0 = g0 + j, r1 = g1 - j;
             for (int it = tid; it < items; it += kThreads) {
-                const int sg = it / wpr, c = it - sg * wpr;
-                const int ra = r0 + sg * rows / segs, rb = r0 + (sg + 1) * rows / segs;
+                int sg = my_sg, c = my_c, ra = my_ra, rb = my_rb;
+                if (it != tid) {  // widths beyond 1024 words: more than one item per thread
+                    sg = it / wpr;
+                    c = it - sg * wpr;
+                    ra = g0 + sg * (g1 - g0) / segs;
+                    rb = g0 + (sg + 1) * (g1 - g0) / segs;
+                }
+                ra = ra < r0 ? r0 : ra;
+                rb = rb > r1 ? r1 : rb;
                 if (ra >= rb) continue;
                 uint32_t sP, cP, sC, cC, sN, cN;
                 lds_row<BOUNDED>(A + (ra - 1) * wpr, wpr, c, sP, cP);
