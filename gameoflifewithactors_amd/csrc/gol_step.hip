@@ -67,6 +67,9 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 #ifndef GOL_STAMP
 #define GOL_STAMP 0
 #endif
+#ifndef GOL_PRIO
+#define GOL_PRIO 0
+#endif
 #if GOL_STAMP
 static constexpr int kStamps = 1 << 16;
 __device__ unsigned long long g_stamps[2][kStamps];
@@ -487,6 +490,14 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         sy = gw / a.nstrips;
     }
     W w(src, dst, a, lane, sx, sy, role);
+#if GOL_PRIO
+    // The split gives the oldest wave of a SIMD group the largest share because VALU issue favours it.  That
+    // order is "priority, then age" (MI355X_MICROARCH.md "Two waves per SIMD"); a static priority by role makes
+    // it the code's choice instead of the dispatch's.
+    if (role == 0) __builtin_amdgcn_s_setprio(3);
+    else if (role == 1) __builtin_amdgcn_s_setprio(2);
+    else if (role == 2) __builtin_amdgcn_s_setprio(1);
+#endif
 #if GOL_STAMP
     const int64_t stamp_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t stamp_t0 = __builtin_amdgcn_s_memrealtime();
