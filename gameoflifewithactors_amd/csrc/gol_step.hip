@@ -67,9 +67,6 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 #ifndef GOL_STAMP
 #define GOL_STAMP 0
 #endif
-#ifndef GOL_PRIO
-#define GOL_PRIO 0
-#endif
 #if GOL_STAMP
 static constexpr int kStamps = 1 << 16;
 __device__ unsigned long long g_stamps[2][kStamps];
@@ -490,14 +487,6 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         sy = gw / a.nstrips;
     }
     W w(src, dst, a, lane, sx, sy, role);
-#if GOL_PRIO
-    // The split gives the oldest wave of a SIMD group the largest share because VALU issue favours it.  That
-    // order is "priority, then age" (MI355X_MICROARCH.md "Two waves per SIMD"); a static priority by role makes
-    // it the code's choice instead of the dispatch's.
-    if (role == 0) __builtin_amdgcn_s_setprio(3);
-    else if (role == 1) __builtin_amdgcn_s_setprio(2);
-    else if (role == 2) __builtin_amdgcn_s_setprio(1);
-#endif
 #if GOL_STAMP
     const int64_t stamp_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t stamp_t0 = __builtin_amdgcn_s_memrealtime();
@@ -664,7 +653,7 @@ int stream_wpb(int k, int ilv, bool bounded, bool wrap) {
 // equal segments it finishes early and leaves the younger alone at the single-wave issue rate
 // (tools/tail.py: 65536^2, K = 16 -- waves 0-3 of every workgroup busy 489 us, waves 4-7 747 us).
 // GOL_SPLIT=<fraction> overrides (experiments); 0 disables.
-int stream_pair_split(int k, int ilv) {
+int stream_pair_split(int k, int ilv, bool bounded) {
     static const int env = [] {
         const char* e = std::getenv("GOL_SPLIT");
         return e ? (int)(std::atof(e) * 65536.0) : -1;
@@ -674,6 +663,9 @@ int stream_pair_split(int k, int ilv) {
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
     // (12, 2) runs 12-wave workgroups at 3 waves/SIMD: three-way groups (profiles/r1/w12_sweep*.log)
+    // Bounded (16, 2) falls off a cliff above 0.6: 98.8k GCUPS at 0.6, 85.4k at 0.7, with the same
+    // instruction counts (profiles/r2/prio_split_j.log, split_bounded_i.log); the torus variants peak at 0.7.
+    if (bounded && ilv == 2 && k == 16) return (int)(0.60 * 65536);
     if (ilv == 1 && k >= 24) return (int)(0.60 * 65536);
     if (ilv == 2 && k == 12) return (int)(0.70 * 65536);
     if (ilv == 2 && k >= 16) return (int)(0.72 * 65536);
@@ -715,7 +707,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         const char* e = std::getenv("GOL_SEG_ROWS");
         return e ? std::atoll(e) : 0LL;
     }();
-    a.split = stream_pair_split(k, a.ilv);
+    a.split = stream_pair_split(k, a.ilv, bounded);
     a.nstrips = stream_strips(a.words, a.ilv, k, bounded);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
