@@ -166,16 +166,27 @@ constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
-// Cooperative LDS-band pass (gol_coop.hip) for packed ilv-1 boards above the LDS-resident cut-over and below
-// this many cells; GOL_COOP=0 disables it, GOL_COOP_MAX_CELLS moves the cut-over (A/B runs; read per call).
+// Cooperative register-band pass (gol_coop.hip) for packed boards above the LDS-resident cut-over and up to
+// this many cells, up to 8192 wide: 512^2 0.87 vs 1.49 us/generation on the streaming pass, 2048^2 0.69 vs 1.48,
+// 4096^2 1.14 vs 1.62 (profiles/r2/small_coop_k.log).  GOL_COOP=0 disables it, GOL_COOP_MAX_CELLS moves the
+// cut-over (A/B runs; read per call).
 constexpr int64_t kCoopMaxCells = (int64_t)1 << 25;
+bool coop_enabled() {
+    const char* e = std::getenv("GOL_COOP");
+    return !(e && e[0] == '0');
+}
 constexpr int kCoopFlagWords = 1024;            // flags of up to 1023 bands ...
 constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
 
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
     const int env = pick_ilv(width);
-    if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) return 1;
+    if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) {
+        // the cooperative pass sums interleaved blocks with 2 funnel shifts per block instead of 2 per word
+        const int m = width % 32 == 0 ? gol::coop_m(width / 32) : 0;
+        if (coop_enabled() && m > 1 && width * height > kResidentMaxCells) return m;
+        return 1;
+    }
     return env;
 }
 // Boards up to this many cells run every gol_step call as ONE launch of the LDS-resident kernel
@@ -216,6 +227,8 @@ struct gol_board {
     int cur = 0;
     unsigned long long* acc = nullptr;  // device scratch accumulator
     unsigned* coop = nullptr;           // cooperative pass: per-band flags + error word (allocated on first use)
+    uint32_t* coop_xch = nullptr;       // cooperative pass: exchange rows (allocated on first use)
+    int64_t coop_xch_words = 0;
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -339,16 +352,21 @@ bool use_wave_resident(const gol_board* b) {
     return gol::wave_resident_rpl(b->W, b->H) > 0 && (!b->packed || b->ilv == 1);
 }
 
+// Generations per hand-off of the cooperative pass: GOL_COOP_K if set (A/B runs), else the board's
+// temporal-block cap, at most gol::coop_k().
+int coop_depth(const gol_board* b) {
+    if (std::getenv("GOL_COOP_K")) return gol::coop_k();
+    return b->tblock < gol::coop_k() ? b->tblock : gol::coop_k();
+}
+
 bool use_coop(const gol_board* b) {
-    // opt-in until it beats the streaming pass: 4096^2 ran 2.2-2.6 us/generation against 1.6 streaming
-    // (profiles/r2/small_coop*.log)
-    const char* e = std::getenv("GOL_COOP");
-    if (!e || e[0] != '1') return false;
+    if (!coop_enabled() || !b->packed) return false;
     const char* m = std::getenv("GOL_COOP_MAX_CELLS");
     const int64_t maxc = m ? (int64_t)std::atoll(m) : kCoopMaxCells;
-    int nwg = 0, B = 0;
-    return b->packed && b->ilv == 1 && b->W * b->H <= maxc && gol::coop_plan(b->W, b->H, gol::coop_k(), &nwg, &B) &&
-           nwg < kCoopFlagWords;
+    const int cm = gol::coop_m(b->W / 32);
+    int nwg = 0, B = 0, R = 0;
+    return (b->ilv == 1 || b->ilv == cm) && b->W * b->H <= maxc &&
+           gol::coop_plan(b->W, b->H, coop_depth(b), &nwg, &B, &R) && nwg < kCoopFlagWords;
 }
 
 int step_impl(gol_board* b, int64_t gens) {
@@ -388,13 +406,27 @@ int step_impl(gol_board* b, int64_t gens) {
             GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
             GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
         }
+        int nwg = 0, B = 0, R = 0;
+        const int k = coop_depth(b);
+        (void)gol::coop_plan(b->W, b->H, k, &nwg, &B, &R);
+        const int64_t need = gol::coop_xch_words(b->W, nwg, k);
+        if (need > b->coop_xch_words) {
+            if (b->coop_xch) {
+                GOL_HIP(hipStreamSynchronize(b->stream));
+                GOL_HIP(hipFree(b->coop_xch));
+                b->coop_xch = nullptr;
+                b->coop_xch_words = 0;
+            }
+            GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
+            b->coop_xch_words = need;
+        }
         while (gens > 0) {
             const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
-            GOL_HIP(gol::launch_coop_pass(b->words(0), b->words(1), b->cur, b->W, b->H, b->pitch, g,
+            GOL_HIP(gol::launch_coop_pass(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, b->ilv, k, g,
                                           b->boundary == GOL_BOUNDED, b->coop,
-                                          reinterpret_cast<int*>(b->coop + kCoopErrWord), b->stream));
-            const int64_t k = gol::coop_k();
-            if (((g + k - 1) / k) % 2) b->cur ^= 1;  // each block of <= k generations flips the buffers
+                                          reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
+                                          b->coop_xch_words, b->stream));
+            b->cur ^= 1;
             b->generation += g;
             gens -= g;
         }
@@ -447,6 +479,7 @@ void free_board(gol_board* b) {
         if (p) (void)hipFree(p);
     if (b->acc) (void)hipFree(b->acc);
     if (b->coop) (void)hipFree(b->coop);
+    if (b->coop_xch) (void)hipFree(b->coop_xch);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }

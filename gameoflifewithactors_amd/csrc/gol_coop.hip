@@ -1,26 +1,30 @@
-// gol_coop.hip -- persistent, LDS-banded pass for mid-size boards (BASELINE config 2: 4096^2) on gfx950.
+// gol_coop.hip -- persistent register-band pass for mid-size boards (BASELINE config 2: 4096^2) on gfx950.
 //
-// A 4096^2 board is 2 MiB packed: too large for one CU's LDS (gol_resident.hip), too small to fill the chip
-// with the streaming pass (gol_step.hip), where each wave is one long serial chain per launch.  Here ONE
-// workgroup per CU stays resident for a whole gol_step call and owns a band of B rows.  Per block of k
-// generations (k <= K, B >= k) it
-//   1. loads its band plus k halo rows on each side (rows wrap on a torus, GameOfLifeDriver.fs:21-25; rows
-//      beyond a bounded board are dead, Script.fsx:6-13) from the board buffer into LDS,
-//   2. runs k synchronous B3/S23 generations (GameOfLifeLogic.fs:59-63) between two LDS buffers with one
-//      workgroup barrier per generation (the halo shrinks by a row per generation; the band stays exact),
-//   3. stores its band to the other board buffer and publishes "block done" to its two neighbours,
-// and before the next block waits only for its two neighbour bands (their halo rows, and that they have
-// finished reading the rows it is about to overwrite).  No grid barrier, one launch per call.
+// A 4096^2 board is 2 MiB packed: too large for one CU (gol_resident.hip), too small to fill the chip with the
+// streaming pass (gol_step.hip), where each wave is one long serial chain per launch.  Here ONE workgroup of 16
+// waves per CU stays resident for a whole gol_step call and owns a band of B rows, held in VGPRs:
 //
-// The band stays in LDS for the whole call; only its first and last k rows are handed to the neighbours per
-// block.  Hand-off protocol (MI355X_MICROARCH.md "Valid forms", first row of the sc1 table: hipMalloc, one
-// workgroup per CU): the edge rows are stored write-through (sc1), every storing wave drains them
-// (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the band's flag (sc1); the consumer's one
-// lane polls the flags with sc1 loads, a workgroup barrier, and every wave loads the rows with sc1 loads --
-// no release / acquire fences (they write back / invalidate whole caches: MI355X_MICROARCH.md
-// "publish-large").  Residency: the grid is one workgroup per CU, each asking for more than
-// half of the CU's LDS, launched cooperatively (the runtime rejects a grid that cannot be co-resident); every
-// spin is bounded and a timed-out wait raises an error word the host checks on the next synchronisation.
+//   local row i = global row y0 - K + i, i in [0, B + 2K): K halo rows above, the band, K halo rows below;
+//   wave v holds local rows [v R, v R + R), lane l the words [l M, l M + M) of each (ilv-1 board, W <= 8192).
+//
+// Per generation (GameOfLifeLogic.fs:59-63, synchronous as under the Reset->State barrier) each wave writes its
+// first and last row to LDS, one workgroup barrier, reads the row above its first and below its last, and
+// steps its rows in registers: horizontal neighbours in the lane and from the adjacent lanes (DPP; the x-wrap
+// of a torus, GameOfLifeDriver.fs:21-25, by DPP rotate or readlane), the rule from gol_bitlogic.h.  Rows
+// outside a bounded board stay dead (Script.fsx:6-13).  Per block of k <= K generations the valid rows shrink
+// by one per side and generation, so the band stays exact; between blocks only the band's first and last K rows
+// leave the CU.
+//
+// Hand-off between neighbour bands (MI355X_MICROARCH.md "Valid forms", first row of the sc1 table: hipMalloc,
+// one workgroup per CU): the edge rows go to a dedicated exchange buffer with write-through (sc1) stores, every
+// storing wave drains them (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the band's block
+// counter (sc1); the consumer's one lane polls its two neighbours' counters with sc1 loads, a workgroup barrier,
+// and the waves holding halo rows load them with sc1 loads.  Every load of an exchange-buffer byte is an sc1
+// load, and the board buffers themselves are only read at the start and written at the end (kernel boundaries
+// order those).  The exchange buffer is double-buffered by block parity: a band rewrites parity p after both
+// neighbours have published the next block, which they do after reading parity p.  Residency: the grid is one
+// workgroup per CU (LDS request above half the CU's), launched cooperatively; every spin is bounded, and a
+// timed-out wait raises an error word the host checks on the next synchronisation.
 #include "gol_internal.h"
 #include "gol_bitlogic.h"
 
@@ -29,33 +33,25 @@
 namespace gol {
 namespace {
 
-constexpr int kThreads = 1024;
-constexpr int kMinLds = 96 * 1024;  // > half the CU's 160 KiB: one workgroup per CU
-constexpr unsigned kSpinLimit = 1u << 22;  // ~ seconds: a wait this long means a band is not resident
+constexpr int kWaves = 16;                 // waves per workgroup: 4 per SIMD
+constexpr int kThreads = 64 * kWaves;
+constexpr int kMinLds = 96 * 1024;         // > half the CU's 160 KiB: one workgroup per CU
+constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident
 
 struct CoopArgs {
-    uint32_t* buf[2];
-    int64_t pitch;   // words per buffer row
-    int wpr;         // words per board row (W / 32)
-    int H;           // board rows
-    int B;           // rows of the largest band (LDS sizing)
-    int nwg;         // bands (= workgroups)
-    int K;           // generations per block (<= B)
+    const uint32_t* src;  // board at launch
+    uint32_t* dst;        // board after `gens` generations
+    uint32_t* xch;        // exchange rows: [2 parity][nwg][2 (band top, band bottom)][K][nw]
+    int64_t pitch;        // words per board row
+    int nw;               // words per row (W / 32)
+    int nl;               // lanes holding words (nw / M)
+    int H;                // board rows
+    int nwg;              // bands (= workgroups)
+    int K;                // generations per block (<= every band's height)
     int gens;
-    int cur;         // buffer holding the board at launch
-    unsigned* flags; // per band: blocks completed (zeroed before the launch)
-    int* err;        // set to 1 by a timed-out wait
+    unsigned* flags;      // per band: blocks published (zeroed before the launch)
+    int* err;             // set to 1 by a timed-out wait
 };
-
-// Horizontal 3-sums of word c of an LDS row (ilv-1 layout).
-template <bool BOUNDED>
-__device__ __forceinline__ uint32_t lds_row(const uint32_t* row, int wpr, int c, uint32_t& s, uint32_t& cy) {
-    const uint32_t m = row[c];
-    const uint32_t l = (BOUNDED && c == 0) ? 0u : row[c == 0 ? wpr - 1 : c - 1];
-    const uint32_t r = (BOUNDED && c == wpr - 1) ? 0u : row[c == wpr - 1 ? 0 : c + 1];
-    row_sum(l, m, r, s, cy);
-    return m;
-}
 
 __device__ __forceinline__ bool wait_flag(const unsigned* f, unsigned target) {
     for (unsigned i = 0; i < kSpinLimit; i++) {
@@ -65,7 +61,7 @@ __device__ __forceinline__ bool wait_flag(const unsigned* f, unsigned target) {
     return false;
 }
 
-// sc1 (write-through / L2-coherent) word store and load for the handed-off edge rows
+// sc1 (write-through / L2-coherent) word store and load for the handed-off rows
 __device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -73,119 +69,176 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool BOUNDED>
-__global__ __launch_bounds__(kThreads) void gol_coop_pass(CoopArgs a) {
-    extern __shared__ uint32_t lds[];
+// Word of the lane to the left / right.  FULL (all 64 lanes hold words): DPP rotate on a torus, DPP shift with
+// zero fill on a bounded board.  Otherwise DPP shift (idle lanes hold zeros, which is a bounded board's dead
+// edge) and on a torus the wrap between lane nl - 1 and lane 0 by readlane.
+template <bool BOUNDED, bool FULL>
+__device__ __forceinline__ uint32_t from_left(uint32_t v, int lane, int nl) {
+    if (FULL && !BOUNDED) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
+    uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);                  // wave_shr:1
+    if (!BOUNDED) {
+        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)v, nl - 1);
+        r = lane == 0 ? last : r;
+    }
+    return r;
+}
+template <bool BOUNDED, bool FULL>
+__device__ __forceinline__ uint32_t from_right(uint32_t v, int lane, int nl) {
+    if (FULL && !BOUNDED) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
+    uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);                  // wave_shl:1
+    if (!BOUNDED) {
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+        r = lane == nl - 1 ? first : r;
+    }
+    return r;
+}
+
+// Horizontal 3-sums of this lane's M words of one row: M consecutive words of an ilv-1 board (2 funnel shifts
+// per word), or one interleaved block of an ilv-M board (gol_layout.h: 2 funnel shifts per block).
+template <int M, bool ILV, bool BOUNDED, bool FULL>
+__device__ __forceinline__ void lane_row_sum(const uint32_t (&r)[M], int lane, int nl, uint32_t (&s)[M],
+                                             uint32_t (&c)[M]) {
+    const uint32_t left = from_left<BOUNDED, FULL>(r[M - 1], lane, nl);
+    const uint32_t right = from_right<BOUNDED, FULL>(r[0], lane, nl);
+    if (ILV) {
+        row_sum_block<M>(r, left, right, s, c);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < M; j++) row_sum(j == 0 ? left : r[j - 1], r[j], j == M - 1 ? right : r[j + 1], s[j], c[j]);
+}
+
+template <int M, int R, bool ILV, bool BOUNDED, bool FULL>
+__global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
+    extern __shared__ uint32_t xs[];  // [2 parity][kWaves][2 (first row, last row)][M][64 lanes]
     const int band = blockIdx.x;
-    const int tid = threadIdx.x;
-    // balanced bands: every band has at least K rows, so a k-row halo comes from ONE neighbour band
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int y0 = (int)((int64_t)a.H * band / a.nwg);
     const int y1 = (int)((int64_t)a.H * (band + 1) / a.nwg);
-    const int own = y1 - y0;
-    const int wpr = a.wpr;
+    const int B = y1 - y0;
     const int K = a.K;
-    const int stride = (a.B + 2 * K) * wpr;  // words per LDS buffer; local row K + i = global row y0 + i
-    // neighbour bands (a bounded board's end bands have one; a one-band torus is its own neighbour)
+    const int L = B + 2 * K;  // local rows
+    const int r0 = wv * R;    // this wave's first local row
+    const int nl = a.nl;
+    const bool lane_on = FULL || lane < nl;  // full rows: every lane holds words
+    const int col = lane * M;  // this lane's first word
     const int up = band > 0 ? band - 1 : (BOUNDED ? -1 : a.nwg - 1);
     const int dn = band + 1 < a.nwg ? band + 1 : (BOUNDED ? -1 : 0);
-    const int segs = wpr >= kThreads ? 1 : kThreads / wpr;  // row segments per column
-    const int items = wpr * segs;
-    const int my_sg = tid / wpr, my_c = tid - my_sg * wpr;  // this thread's first item
-    const int nblk = (a.gens + K - 1) / K;
-    auto wrap = [&](int gy) { return gy < 0 ? gy + a.H : (gy >= a.H ? gy - a.H : gy); };
+    auto gy_of = [&](int i) { return y0 - K + i; };
     auto on_board = [&](int gy) { return gy >= 0 && gy < a.H; };
-    uint32_t* A = lds;  // the band (+ halo) at the start of a block
-    uint32_t* Bf = lds + stride;
-    // the band and K halo rows per side, once, from the board
-    {
-        const uint32_t* src = a.buf[a.cur];
-        const int n = own + 2 * K;
-        for (int i = tid; i < n * wpr; i += kThreads) {
-            const int r = i / wpr, c = i - r * wpr;
-            const int gy = y0 - K + r;
-            uint32_t v = 0;
-            if (on_board(gy) || !BOUNDED) v = src[(int64_t)wrap(gy) * a.pitch + c];
-            A[r * wpr + c] = v;
+    auto wrap = [&](int gy) { return gy < 0 ? gy + a.H : (gy >= a.H ? gy - a.H : gy); };
+    auto xrow = [&](int parity, int b, int side, int i) {  // exchange row (band b's top / bottom K rows, row i)
+        return a.xch + ((((int64_t)parity * a.nwg + b) * 2 + side) * K + i) * a.nw;
+    };
+
+    // ---- the band and its halo from the board (plain loads: the board buffers are not handed off in-kernel)
+    uint32_t w[R][M];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        const int gy = gy_of(r0 + i);
+#pragma unroll
+        for (int j = 0; j < M; j++) w[i][j] = 0;
+        if (r0 + i < L && lane_on && (!BOUNDED || on_board(gy))) {
+            const uint32_t* row = a.src + (int64_t)wrap(gy) * a.pitch + col;
+#pragma unroll
+            for (int j = 0; j < M; j++) w[i][j] = row[j];
         }
-        __syncthreads();
     }
-    int x = a.cur;  // board buffer the latest hand-off went to
+
+    const int nblk = (a.gens + K - 1) / K;
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
         if (blk > 0) {
-            // the neighbours finished block blk - 1: their edge rows are in buf[x] (write-through), and
-            // they have read ours from the buffer we are about to write (blk + 1 alternates)
-            if (tid == 0) {
+            // neighbours published block blk - 1 (parity (blk - 1) & 1): their edge rows become our halo
+            if (threadIdx.x == 0) {
                 bool ok = true;
                 if (up >= 0) ok = wait_flag(a.flags + up, (unsigned)blk) && ok;
                 if (dn >= 0) ok = wait_flag(a.flags + dn, (unsigned)blk) && ok;
                 if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();
-            // halo rows: k above (the up band's last rows), k below (the down band's first rows)
-            const uint32_t* src = a.buf[x];
-            for (int i = tid; i < 2 * k * wpr; i += kThreads) {
-                const int r = i / wpr, c = i - r * wpr;
-                const int lr = r < k ? K - k + r : K + own + (r - k);  // local row
-                const int gy = y0 - K + lr;
-                uint32_t v = 0;
-                if (on_board(gy) || !BOUNDED) v = ld_sc1(src + (int64_t)wrap(gy) * a.pitch + c);
-                A[lr * wpr + c] = v;
+            const int par = (blk - 1) & 1;
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const int li = r0 + i;
+                const uint32_t* src = nullptr;
+                if (li < K && up >= 0) src = xrow(par, up, 1, li);                       // up band's bottom rows
+                else if (li >= K + B && li < L && dn >= 0) src = xrow(par, dn, 0, li - K - B);  // dn band's top rows
+                if (src && lane_on) {
+#pragma unroll
+                    for (int j = 0; j < M; j++) w[i][j] = ld_sc1(src + col + j);
+                }
             }
-            __syncthreads();
         }
-        // k generations in LDS: generation j writes local rows [K - k + 1 + j, K + own + k - 1 - j).  Each
-        // item's row segment is fixed for the block (split of generation 0's rows) and clipped per generation:
-        // no division in the generation loop.
-        const int g0 = K - k + 1, g1 = K + own + k - 1;
-        const int my_ra = g0 + my_sg * (g1 - g0) / segs, my_rb = g0 + (my_sg + 1) * (g1 - g0) / segs;
+        // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j)
         for (int j = 0; j < k; j++) {
-            const int r0 = g0 + j, r1 = g1 - j;
-            for (int it = tid; it < items; it += kThreads) {
-                int sg = my_sg, c = my_c, ra = my_ra, rb = my_rb;
-                if (it != tid) {  // widths beyond 1024 words: more than one item per thread
-                    sg = it / wpr;
-                    c = it - sg * wpr;
-                    ra = g0 + sg * (g1 - g0) / segs;
-                    rb = g0 + (sg + 1) * (g1 - g0) / segs;
-                }
-                ra = ra < r0 ? r0 : ra;
-                rb = rb > r1 ? r1 : rb;
-                if (ra >= rb) continue;
-                uint32_t sP, cP, sC, cC, sN, cN;
-                lds_row<BOUNDED>(A + (ra - 1) * wpr, wpr, c, sP, cP);
-                uint32_t mC = lds_row<BOUNDED>(A + ra * wpr, wpr, c, sC, cC);
-                for (int r = ra; r < rb; r++) {
-                    const uint32_t mN = lds_row<BOUNDED>(A + (r + 1) * wpr, wpr, c, sN, cN);
-                    uint32_t v = life_next(sP, cP, sC, cC, sN, cN, mC);
-                    if (BOUNDED && !on_board(y0 - K + r)) v = 0u;  // dead outside the board at every generation
-                    Bf[r * wpr + c] = v;
-                    sP = sC, cP = cC, sC = sN, cC = cN, mC = mN;
-                }
+            const int par = j & 1;
+            uint32_t* slot = xs + (par * kWaves) * 2 * M * 64;
+#pragma unroll
+            for (int t = 0; t < M; t++) {
+                slot[((wv * 2 + 0) * M + t) * 64 + lane] = w[0][t];
+                slot[((wv * 2 + 1) * M + t) * 64 + lane] = w[R - 1][t];
             }
             __syncthreads();
-            uint32_t* t = A;
-            A = Bf;
-            Bf = t;
+            const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
+            if (r0 >= hi || r0 + R <= lo) continue;  // wave-uniform: none of this wave's rows is produced
+            uint32_t above[M], below[M];
+#pragma unroll
+            for (int t = 0; t < M; t++) {
+                above[t] = wv > 0 ? slot[(((wv - 1) * 2 + 1) * M + t) * 64 + lane] : 0u;
+                below[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane] : 0u;
+            }
+            uint32_t sP[M], cP[M], sC[M], cC[M], sN[M], cN[M];
+            lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sP, cP);
+            lane_row_sum<M, ILV, BOUNDED, FULL>(w[0], lane, nl, sC, cC);
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                lane_row_sum<M, ILV, BOUNDED, FULL>(i + 1 < R ? w[i + 1] : below, lane, nl, sN, cN);
+                const bool dead = BOUNDED && !on_board(gy_of(r0 + i));  // dead outside the board at every generation
+#pragma unroll
+                for (int t = 0; t < M; t++) {
+                    const uint32_t v = life_next(sP[t], cP[t], sC[t], cC[t], sN[t], cN[t], w[i][t]);
+                    w[i][t] = dead || !lane_on ? 0u : v;
+                    sP[t] = sC[t], cP[t] = cC[t], sC[t] = sN[t], cC[t] = cN[t];
+                }
+            }
         }
         if (blk + 1 == nblk) break;
-        // hand-off: the band's first and last k rows, write-through, to the other board buffer
-        x ^= 1;
-        uint32_t* dst = a.buf[x];
-        for (int i = tid; i < 2 * k * wpr; i += kThreads) {
-            const int r = i / wpr, c = i - r * wpr;
-            const int lr = r < k ? K + r : K + own - k + (r - k);
-            st_sc1(dst + (int64_t)(y0 - K + lr) * a.pitch + c, A[lr * wpr + c]);
+        // ---- hand-off: the band's first and last K rows to exchange parity blk & 1, write-through
+        const int par = blk & 1;
+        bool stored = false;
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const int li = r0 + i;
+            // a band shorter than 2K rows has rows in both ranges: each goes to both sides
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const int e = side == 0 ? li - K : li - B;  // row index within the band's top / bottom K rows
+                if (e < 0 || e >= K) continue;
+                stored = true;
+                uint32_t* dst = xrow(par, band, side, e);
+                if (lane_on) {
+#pragma unroll
+                    for (int t = 0; t < M; t++) st_sc1(dst + col + t, w[i][t]);
+                }
+            }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores complete ...
-        __syncthreads();                                   // ... before one lane publishes for all
-        if (tid == 0) __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (stored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores complete ...
+        __syncthreads();                                                // ... before one lane publishes for all
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // the whole band to the result buffer (the host flips the board buffer once per block)
-    uint32_t* dst = a.buf[a.cur ^ (nblk & 1)];
-    for (int i = tid; i < own * wpr; i += kThreads) {
-        const int r = i / wpr, c = i - r * wpr;
-        dst[(int64_t)(y0 + r) * a.pitch + c] = A[(K + r) * wpr + c];
+    // ---- the band to the result buffer
+    if (!lane_on) return;
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        const int li = r0 + i;
+        if (li >= K && li < K + B) {
+            uint32_t* row = a.dst + (int64_t)gy_of(li) * a.pitch + col;
+#pragma unroll
+            for (int t = 0; t < M; t++) row[t] = w[i][t];
+        }
     }
 }
 
@@ -199,58 +252,119 @@ int coop_cus() {
     return cus;
 }
 
+constexpr int kRows[] = {1, 2, 3, 4, 6, 8};  // rows per wave instantiated
+
+template <int M, int R, bool ILV>
+const void* kernel_mri(bool bounded, bool full) {
+    if (bounded)
+        return full ? (const void*)&gol_band_pass<M, R, ILV, true, true> : (const void*)&gol_band_pass<M, R, ILV, true, false>;
+    return full ? (const void*)&gol_band_pass<M, R, ILV, false, true> : (const void*)&gol_band_pass<M, R, ILV, false, false>;
+}
+
+template <int M>
+const void* kernel_m(int r, bool ilv, bool bounded, bool full) {
+    if (M > 1 && ilv) {  // interleaved boards (ilv == M)
+        switch (r) {
+            case 1: return kernel_mri<M, 1, true>(bounded, full);
+            case 2: return kernel_mri<M, 2, true>(bounded, full);
+            case 3: return kernel_mri<M, 3, true>(bounded, full);
+            case 4: return kernel_mri<M, 4, true>(bounded, full);
+            case 6: return kernel_mri<M, 6, true>(bounded, full);
+            case 8: return kernel_mri<M, 8, true>(bounded, full);
+        }
+        return nullptr;
+    }
+    switch (r) {
+        case 1: return kernel_mri<M, 1, false>(bounded, full);
+        case 2: return kernel_mri<M, 2, false>(bounded, full);
+        case 3: return kernel_mri<M, 3, false>(bounded, full);
+        case 4: return kernel_mri<M, 4, false>(bounded, full);
+        case 6: return kernel_mri<M, 6, false>(bounded, full);
+        case 8: return kernel_mri<M, 8, false>(bounded, full);
+    }
+    return nullptr;
+}
+
 }  // namespace
 
-// Generations per block: GOL_COOP_K overrides (A/B), default 8.
+// Generations per block (the board's tblock_k caps it): GOL_COOP_K overrides (A/B), default 8.
 int coop_k() {
     const char* e = std::getenv("GOL_COOP_K");
     const int k = e ? std::atoi(e) : 8;
     return k >= 1 && k <= 64 ? k : 8;
 }
 
-bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B) {
+// Words per lane for a row of nw words (0: the width does not fit one wave).
+int coop_m(int64_t nw) {
+    const int m = nw <= 64 ? 1 : (nw <= 128 ? 2 : 4);
+    return nw <= 256 && nw % m == 0 ? m : 0;
+}
+
+// Rows per wave at least: GOL_COOP_R (A/B; fewer, taller wave slices re-sum fewer neighbour rows), default 1.
+static int coop_min_rows() {
+    const char* e = std::getenv("GOL_COOP_R");
+    const int r = e ? std::atoi(e) : 1;
+    return r >= 1 && r <= 8 ? r : 1;
+}
+
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R) {
     const int cus = coop_cus();
-    if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1) return false;
-    const int64_t wpr = W / 32;
-    // balanced bands of >= k rows each (a k-row halo then comes from one neighbour band), one per CU at most
+    if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1 || !coop_m(W / 32)) return false;
+    // balanced bands of >= k rows each (a k-row halo then comes from ONE neighbour band), one per CU at most
     int64_t n = H / k < cus ? H / k : cus;
     if (n < 1) return false;
     const int64_t b = (H + n - 1) / n;  // the largest band
-    if (2 * (b + 2 * k) * wpr * 4 > 160 * 1024) return false;
+    int64_t rows = (b + 2 * k + kWaves - 1) / kWaves;  // rows per wave
+    if (rows < coop_min_rows()) rows = coop_min_rows();
+    int r = 0;
+    for (int c : kRows)
+        if (c >= rows) {
+            r = c;
+            break;
+        }
+    if (!r) return false;
     *nwg = (int)n;
     *B = (int)b;
+    if (R) *R = r;
     return true;
 }
 
-hipError_t launch_coop_pass(uint32_t* buf0, uint32_t* buf1, int cur, int64_t W, int64_t H, int64_t pitch,
-                            int64_t gens, bool bounded, unsigned* flags, int* err, hipStream_t s) {
-    const int k = coop_k();
-    int nwg = 0, B = 0;
-    if (!coop_plan(W, H, k, &nwg, &B) || gens < 1 || gens > INT32_MAX || pitch < W / 32) return hipErrorInvalidValue;
+int64_t coop_xch_words(int64_t W, int nwg, int k) { return (int64_t)2 * nwg * 2 * k * (W / 32); }
+
+hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
+                            int64_t gens, bool bounded, unsigned* flags, int* err, uint32_t* xch, int64_t xch_words,
+                            hipStream_t s) {
+    int nwg = 0, B = 0, R = 0;
+    if (!coop_plan(W, H, k, &nwg, &B, &R) || gens < 1 || gens > INT32_MAX || pitch < W / 32 ||
+        coop_xch_words(W, nwg, k) > xch_words)
+        return hipErrorInvalidValue;
+    const int nw = (int)(W / 32);
+    const int M = coop_m(nw);
+    if (ilv != 1 && ilv != M) return hipErrorInvalidValue;
     CoopArgs a;
-    a.buf[0] = buf0;
-    a.buf[1] = buf1;
+    a.src = src;
+    a.dst = dst;
+    a.xch = xch;
     a.pitch = pitch;
-    a.wpr = (int)(W / 32);
+    a.nw = nw;
+    a.nl = nw / M;
     a.H = (int)H;
-    a.B = B;
     a.nwg = nwg;
     a.K = k;
     a.gens = (int)gens;
-    a.cur = cur;
     a.flags = flags;
     a.err = err;
-    const size_t need = (size_t)2 * (B + 2 * k) * a.wpr * 4;
+    const bool full = a.nl == 64;
+    const bool il = ilv == M && M > 1;
+    const void* fn = M == 1 ? kernel_m<1>(R, false, bounded, full)
+                            : (M == 2 ? kernel_m<2>(R, il, bounded, full) : kernel_m<4>(R, il, bounded, full));
+    if (!fn) return hipErrorInvalidValue;
+    const size_t need = (size_t)2 * kWaves * 2 * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
     hipError_t e = hipMemsetAsync(flags, 0, (size_t)nwg * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    const void* fn = bounded ? (const void*)&gol_coop_pass<true> : (const void*)&gol_coop_pass<false>;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[bounded]) {
-        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set[bounded] = true;
-    }
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
     void* args[] = {&a};
     return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);
 }

@@ -71,11 +71,15 @@ hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W,
 hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, int64_t gens, bool bounded,
                                  hipStream_t s);
 
-// ---- gol_coop.hip: one workgroup per CU owning a band of rows in LDS, k generations per neighbour hand-off
+// ---- gol_coop.hip: one workgroup per CU owning a band of rows in registers, k generations per neighbour
+// hand-off (boards up to 8192 wide, ilv 1 or ilv = coop_m); the result lands in dst
 int coop_k();
-bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B);
-hipError_t launch_coop_pass(uint32_t* buf0, uint32_t* buf1, int cur, int64_t W, int64_t H, int64_t pitch,
-                            int64_t gens, bool bounded, unsigned* flags, int* err, hipStream_t s);
+int coop_m(int64_t nw);  // words per lane for rows of nw words (0: too wide for the pass)
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R);
+int64_t coop_xch_words(int64_t W, int nwg, int k);  // exchange buffer the pass needs
+hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
+                            int64_t gens, bool bounded, unsigned* flags, int* err, uint32_t* xch, int64_t xch_words,
+                            hipStream_t s);
 
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
 int wave_resident_rpl(int64_t W, int64_t H);  // rows per lane, 0 = the board does not fit

@@ -1,11 +1,13 @@
-"""GPU parity of the cooperative LDS-band pass for mid-size boards (csrc/gol_coop.hip).
+"""GPU parity of the cooperative register-band pass for mid-size boards (csrc/gol_coop.hip).
 
-Packed boards above the LDS-resident cut-over (2^17 cells) and up to 2^25 cells run every gol_step call as one
-persistent launch: one workgroup per CU owns a band of rows in LDS and hands its edge rows to its two
-neighbour bands every k generations.  Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus
-GameOfLifeDriver.fs:21-25; bounded Script.fsx:6-13), the BASELINE config-2 golden checkpoints (4096^2, .NET
-Random seed 42, 10k generations), and the streaming pass on the same board (GOL_COOP=0).  Uneven bands
-(heights that do not divide over the CUs), several block depths (GOL_COOP_K) and split calls are covered.
+Packed boards above the LDS-resident cut-over (2^17 cells), up to 2^25 cells and 8192 wide, run every gol_step
+call as one persistent launch: one workgroup per CU holds a band of rows in registers, exchanges wave-edge
+rows through LDS every generation and hands its K edge rows to its two neighbour bands every K generations.
+Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus GameOfLifeDriver.fs:21-25; bounded
+Script.fsx:6-13), the BASELINE config-2 golden checkpoints (4096^2, .NET Random seed 42, 10k generations), and
+the streaming pass on the same board (GOL_COOP=0).  Uneven bands (heights that do not divide over the CUs),
+bands shorter than two blocks, several block depths (GOL_COOP_K), both word layouts (consecutive words of an
+ilv-1 board, interleaved blocks of an ilv-2 / ilv-4 board) and split calls are covered.
 """
 import json
 import os
@@ -47,13 +49,16 @@ class _Env:
                 os.environ[k] = v
 
 
-def _run(gol, b0, boundary, steps, coop, k=None):
+def _run(gol, b0, boundary, steps, coop, k=None, ilv=0):
     h, w = b0.shape
     env = {"GOL_COOP": "1" if coop else "0"}
     if k:
         env["GOL_COOP_K"] = str(k)
-    with _Env(**env), gol.Board(w, h, boundary) as b:
-        assert b.info()["ilv"] == 1
+    with _Env(**env), gol.Board(w, h, boundary, ilv=ilv) as b:
+        if coop and not ilv and w in (4096, 8192):
+            assert b.info()["ilv"] == w // 2048  # the pass's interleaved layout
+        elif not ilv:
+            assert b.info()["ilv"] == 1
         b.set_cells(b0)
         for g in steps:
             b.step(g)
@@ -69,6 +74,15 @@ def test_coop_matches_oracle_and_streaming(gol, oracle, w, h, boundary):
     want = oracle.c_run(b0, sum(steps), boundary)
     np.testing.assert_array_equal(_run(gol, b0, boundary, steps, coop=True), want)
     np.testing.assert_array_equal(_run(gol, b0, boundary, steps, coop=False), want)
+
+
+@pytest.mark.parametrize("w,h", [(4096, 700), (8192, 300), (2048, 1024)])
+def test_coop_consecutive_words(gol, oracle, w, h):
+    """An ilv-1 board of a width the pass holds as 2 or 4 consecutive words per lane."""
+    b0 = _rand(h, w, w + h)
+    for boundary in (0, 1):
+        want = oracle.c_run(b0, 21, boundary)
+        np.testing.assert_array_equal(_run(gol, b0, boundary, [21], coop=True, ilv=1), want)
 
 
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
