@@ -39,15 +39,18 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tuple = (),
-          step_src: str | None = None, flags: tuple = ()) -> str:
-    """Compile SOURCES for gfx950 into `lib`.  `defines` (e.g. ("GOL_XLANE=0",)) and `step_src` (another
-    revision of gol_step.hip) build A/B variants for experiments."""
+          step_src: str | None = None, flags: tuple = (), alt: dict | None = None) -> str:
+    """Compile SOURCES for gfx950 into `lib`.  `defines` (e.g. ("GOL_XLANE=0",)), `step_src` (another revision
+    of gol_step.hip) and `alt` ({basename: path} of other revisions of any source) build A/B variants for
+    experiments."""
     sources = [step_src or SOURCES[0]] + SOURCES[1:]
+    if alt:
+        sources = [alt.get(os.path.basename(x), x) for x in sources]
     deps = sources + HEADERS + [os.path.abspath(__file__)]
     if not force and not _stale(lib, deps):
         return lib
     objs = []
-    tag = "_".join(d.replace("=", "") for d in defines) + ("_alt" if step_src else "") + ("_fl" if flags else "")
+    tag = "_".join(d.replace("=", "") for d in defines) + ("_alt" if step_src or alt else "") + ("_fl" if flags else "")
     procs = []
     for src in sources:  # compile the translation units in parallel (gol_step.hip dominates)
         obj = os.path.join(CSRC, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")

@@ -175,8 +175,9 @@ bool coop_enabled() {
     const char* e = std::getenv("GOL_COOP");
     return !(e && e[0] == '0');
 }
-constexpr int kCoopFlagWords = 1024;            // flags of up to 1023 bands ...
+constexpr int kCoopFlagWords = 1024;            // bands of one launch at most (one per CU) ...
 constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
+constexpr int64_t kCoopMaxGensPerLaunch = 32768;  // a launch's granule tags count its blocks in 16 bits
 
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
@@ -227,8 +228,9 @@ struct gol_board {
     int cur = 0;
     unsigned long long* acc = nullptr;  // device scratch accumulator
     unsigned* coop = nullptr;           // cooperative pass: per-band flags + error word (allocated on first use)
-    uint32_t* coop_xch = nullptr;       // cooperative pass: exchange rows (allocated on first use)
+    uint32_t* coop_xch = nullptr;       // cooperative pass: hand-off granules (allocated on first use)
     int64_t coop_xch_words = 0;
+    unsigned coop_epoch = 0;            // tag epoch of the last cooperative launch (1..65535)
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -419,11 +421,16 @@ int step_impl(gol_board* b, int64_t gens) {
             }
             GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
             b->coop_xch_words = need;
+            b->coop_epoch = 0xffff;  // forces the clear below: a fresh buffer holds arbitrary tags
         }
         while (gens > 0) {
-            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
+            const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;
+            if (++b->coop_epoch > 0xffff) {  // tags of an earlier epoch could match again: clear the granules
+                GOL_HIP(hipMemsetAsync(b->coop_xch, 0, (size_t)b->coop_xch_words * sizeof(uint32_t), b->stream));
+                b->coop_epoch = 1;
+            }
             GOL_HIP(gol::launch_coop_pass(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, b->ilv, k, g,
-                                          b->boundary == GOL_BOUNDED, b->coop,
+                                          b->boundary == GOL_BOUNDED, b->coop_epoch,
                                           reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
                                           b->coop_xch_words, b->stream));
             b->cur ^= 1;

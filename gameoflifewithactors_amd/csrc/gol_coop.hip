@@ -15,16 +15,17 @@
 // by one per side and generation, so the band stays exact; between blocks only the band's first and last K rows
 // leave the CU.
 //
-// Hand-off between neighbour bands (MI355X_MICROARCH.md "Valid forms", first row of the sc1 table: hipMalloc,
-// one workgroup per CU): the edge rows go to a dedicated exchange buffer with write-through (sc1) stores, every
-// storing wave drains them (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane stores the band's block
-// counter (sc1); the consumer's one lane polls its two neighbours' counters with sc1 loads, a workgroup barrier,
-// and the waves holding halo rows load them with sc1 loads.  Every load of an exchange-buffer byte is an sc1
-// load, and the board buffers themselves are only read at the start and written at the end (kernel boundaries
-// order those).  The exchange buffer is double-buffered by block parity: a band rewrites parity p after both
-// neighbours have published the next block, which they do after reading parity p.  Residency: the grid is one
-// workgroup per CU (LDS request above half the CU's), launched cooperatively; every spin is bounded, and a
-// timed-out wait raises an error word the host checks on the next synchronisation.
+// Hand-off between neighbour bands: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1" and "Valid forms", R2).
+// Every word of the band's first and last K rows goes to a dedicated exchange buffer as ONE 8-byte write-through
+// (sc1) store {word, tag}, tag = launch epoch << 16 | block + 1; the neighbour's lanes poll exactly the granules
+// they need with 8-byte sc1 loads until the tag matches -- no drain, no barrier, no flag, and a torn granule is
+// never accepted because data and tag arrive together.  The exchange buffer is double-buffered by block parity:
+// a band rewrites parity p after both neighbours have published the next block, which they do after reading
+// parity p; the epoch keeps a granule of an earlier launch from matching (the host clears the buffer when the
+// 16-bit epoch wraps).  The board buffers are only read at the start and written at the end (kernel boundaries
+// order those).  Residency: the grid is one workgroup per CU (LDS request above half the CU's), launched
+// cooperatively; every spin is bounded, and a timed-out wait raises an error word the host checks on the next
+// synchronisation.
 #include "gol_internal.h"
 #include "gol_bitlogic.h"
 
@@ -38,10 +39,11 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kMinLds = 96 * 1024;         // > half the CU's 160 KiB: one workgroup per CU
 constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident
 
+
 struct CoopArgs {
     const uint32_t* src;  // board at launch
     uint32_t* dst;        // board after `gens` generations
-    uint32_t* xch;        // exchange rows: [2 parity][nwg][2 (band top, band bottom)][K][nw]
+    uint64_t* xch;        // exchange granules: [2 parity][nwg][2 (band top, band bottom)][K][nw] {word, tag}
     int64_t pitch;        // words per board row
     int nw;               // words per row (W / 32)
     int nl;               // lanes holding words (nw / M)
@@ -49,24 +51,35 @@ struct CoopArgs {
     int nwg;              // bands (= workgroups)
     int K;                // generations per block (<= every band's height)
     int gens;
-    unsigned* flags;      // per band: blocks published (zeroed before the launch)
+    unsigned epoch;       // launch epoch (16 bits) of the granule tags
     int* err;             // set to 1 by a timed-out wait
 };
 
-__device__ __forceinline__ bool wait_flag(const unsigned* f, unsigned target) {
-    for (unsigned i = 0; i < kSpinLimit; i++) {
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-        __builtin_amdgcn_s_sleep(2);
+// A lane's M words of one row as granules {word, tag}, write-through (8-byte sc1 stores)
+template <int M>
+__device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M], unsigned tag) {
+#pragma unroll
+    for (int t = 0; t < M; t++)
+        __hip_atomic_store(p + t, (uint64_t)tag << 32 | w[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// ... and back: poll each granule (8-byte sc1 loads) until its tag matches; false after the spin limit
+template <int M>
+__device__ __forceinline__ bool ld_granules(const uint64_t* p, uint32_t (&w)[M], unsigned tag) {
+    bool ok = true;
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        uint64_t v = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned i = 0; (unsigned)(v >> 32) != tag; i++) {
+            if (i == kSpinLimit) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            v = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        w[t] = (uint32_t)v;
     }
-    return false;
-}
-
-// sc1 (write-through / L2-coherent) word store and load for the handed-off rows
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ok;
 }
 
 // Word of the lane to the left / right.  FULL (all 64 lanes hold words): DPP rotate on a torus, DPP shift with
@@ -110,7 +123,7 @@ __device__ __forceinline__ void lane_row_sum(const uint32_t (&r)[M], int lane, i
 
 template <int M, int R, bool ILV, bool BOUNDED, bool FULL>
 __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
-    extern __shared__ uint32_t xs[];  // [2 parity][kWaves][2 (first row, last row)][M][64 lanes]
+    extern __shared__ uint32_t xs[];  // [2 parity][kWaves][2 (first row, last row)][M][64 lanes], then kWaves counters
     const int band = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -131,6 +144,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     auto xrow = [&](int parity, int b, int side, int i) {  // exchange row (band b's top / bottom K rows, row i)
         return a.xch + ((((int64_t)parity * a.nwg + b) * 2 + side) * K + i) * a.nw;
     };
+    auto tag_of = [&](int blk) { return a.epoch << 16 | (unsigned)(blk + 1); };  // tag of block blk's granules
 
     // ---- the band and its halo from the board (plain loads: the board buffers are not handed off in-kernel)
     uint32_t w[R][M];
@@ -150,64 +164,64 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
         if (blk > 0) {
-            // neighbours published block blk - 1 (parity (blk - 1) & 1): their edge rows become our halo
-            if (threadIdx.x == 0) {
-                bool ok = true;
-                if (up >= 0) ok = wait_flag(a.flags + up, (unsigned)blk) && ok;
-                if (dn >= 0) ok = wait_flag(a.flags + dn, (unsigned)blk) && ok;
-                if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
+            // halo rows: the neighbours' edge rows of block blk - 1 (parity (blk - 1) & 1), polled granule by granule
             const int par = (blk - 1) & 1;
+            bool ok = true;
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const int li = r0 + i;
-                const uint32_t* src = nullptr;
-                if (li < K && up >= 0) src = xrow(par, up, 1, li);                       // up band's bottom rows
+                const uint64_t* src = nullptr;
+                if (li < K && up >= 0) src = xrow(par, up, 1, li);                              // up band's bottom rows
                 else if (li >= K + B && li < L && dn >= 0) src = xrow(par, dn, 0, li - K - B);  // dn band's top rows
-                if (src && lane_on) {
-#pragma unroll
-                    for (int j = 0; j < M; j++) w[i][j] = ld_sc1(src + col + j);
-                }
+                if (src && lane_on) ok = ld_granules<M>(src + col, w[i], tag_of(blk - 1)) && ok;
             }
+            if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j)
+        // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j).  The wave's own row
+        // sums do not depend on the exchange: they are summed between publishing the edge rows and the barrier,
+        // so the barrier wait and the LDS round trip overlap them.
         for (int j = 0; j < k; j++) {
-            const int par = j & 1;
+            const int gen = blk * K + j;  // generation of this launch
+            const int par = gen & 1;      // alternates across blocks too: no barrier separates them
             uint32_t* slot = xs + (par * kWaves) * 2 * M * 64;
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 slot[((wv * 2 + 0) * M + t) * 64 + lane] = w[0][t];
                 slot[((wv * 2 + 1) * M + t) * 64 + lane] = w[R - 1][t];
             }
-            __syncthreads();
             const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
-            if (r0 >= hi || r0 + R <= lo) continue;  // wave-uniform: none of this wave's rows is produced
+            const bool active = r0 < hi && r0 + R > lo;  // wave-uniform: some of this wave's rows are produced
+            uint32_t so[R][M], co[R][M];
+            if (active) {
+#pragma unroll
+                for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+            }
+            __syncthreads();  // a barrier per generation: LDS counters per neighbour wave measured 0.90 vs 0.56 us
+            if (!active) continue;
             uint32_t above[M], below[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 above[t] = wv > 0 ? slot[(((wv - 1) * 2 + 1) * M + t) * 64 + lane] : 0u;
                 below[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane] : 0u;
             }
-            uint32_t sP[M], cP[M], sC[M], cC[M], sN[M], cN[M];
-            lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sP, cP);
-            lane_row_sum<M, ILV, BOUNDED, FULL>(w[0], lane, nl, sC, cC);
+            uint32_t sa[M], ca[M], sb[M], cb[M];
+            lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sa, ca);
+            lane_row_sum<M, ILV, BOUNDED, FULL>(below, lane, nl, sb, cb);
 #pragma unroll
             for (int i = 0; i < R; i++) {
-                lane_row_sum<M, ILV, BOUNDED, FULL>(i + 1 < R ? w[i + 1] : below, lane, nl, sN, cN);
                 const bool dead = BOUNDED && !on_board(gy_of(r0 + i));  // dead outside the board at every generation
 #pragma unroll
                 for (int t = 0; t < M; t++) {
-                    const uint32_t v = life_next(sP[t], cP[t], sC[t], cC[t], sN[t], cN[t], w[i][t]);
+                    const uint32_t v = life_next(i == 0 ? sa[t] : so[i - 1][t], i == 0 ? ca[t] : co[i - 1][t], so[i][t],
+                                                 co[i][t], i == R - 1 ? sb[t] : so[i + 1][t],
+                                                 i == R - 1 ? cb[t] : co[i + 1][t], w[i][t]);
                     w[i][t] = dead || !lane_on ? 0u : v;
-                    sP[t] = sC[t], cP[t] = cC[t], sC[t] = sN[t], cC[t] = cN[t];
                 }
             }
         }
         if (blk + 1 == nblk) break;
-        // ---- hand-off: the band's first and last K rows to exchange parity blk & 1, write-through
+        // ---- hand-off: the band's first and last K rows as granules of parity blk & 1
         const int par = blk & 1;
-        bool stored = false;
 #pragma unroll
         for (int i = 0; i < R; i++) {
             const int li = r0 + i;
@@ -215,19 +229,10 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
 #pragma unroll
             for (int side = 0; side < 2; side++) {
                 const int e = side == 0 ? li - K : li - B;  // row index within the band's top / bottom K rows
-                if (e < 0 || e >= K) continue;
-                stored = true;
-                uint32_t* dst = xrow(par, band, side, e);
-                if (lane_on) {
-#pragma unroll
-                    for (int t = 0; t < M; t++) st_sc1(dst + col + t, w[i][t]);
-                }
+                if (e < 0 || e >= K || !lane_on) continue;
+                st_granules<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
             }
         }
-        if (stored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores complete ...
-        __syncthreads();                                                // ... before one lane publishes for all
-        if (threadIdx.x == 0)
-            __hip_atomic_store(a.flags + band, (unsigned)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- the band to the result buffer
     if (!lane_on) return;
@@ -329,13 +334,13 @@ bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R) {
     return true;
 }
 
-int64_t coop_xch_words(int64_t W, int nwg, int k) { return (int64_t)2 * nwg * 2 * k * (W / 32); }
+int64_t coop_xch_words(int64_t W, int nwg, int k) { return (int64_t)2 * 2 * nwg * 2 * k * (W / 32); }
 
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
-                            int64_t gens, bool bounded, unsigned* flags, int* err, uint32_t* xch, int64_t xch_words,
+                            int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
                             hipStream_t s) {
     int nwg = 0, B = 0, R = 0;
-    if (!coop_plan(W, H, k, &nwg, &B, &R) || gens < 1 || gens > INT32_MAX || pitch < W / 32 ||
+    if (!coop_plan(W, H, k, &nwg, &B, &R) || gens < 1 || gens > 65535 || pitch < W / 32 ||
         coop_xch_words(W, nwg, k) > xch_words)
         return hipErrorInvalidValue;
     const int nw = (int)(W / 32);
@@ -344,7 +349,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     CoopArgs a;
     a.src = src;
     a.dst = dst;
-    a.xch = xch;
+    a.xch = reinterpret_cast<uint64_t*>(xch);
     a.pitch = pitch;
     a.nw = nw;
     a.nl = nw / M;
@@ -352,7 +357,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     a.nwg = nwg;
     a.K = k;
     a.gens = (int)gens;
-    a.flags = flags;
+    a.epoch = epoch & 0xffffu;
     a.err = err;
     const bool full = a.nl == 64;
     const bool il = ilv == M && M > 1;
@@ -361,9 +366,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     if (!fn) return hipErrorInvalidValue;
     const size_t need = (size_t)2 * kWaves * 2 * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
-    hipError_t e = hipMemsetAsync(flags, 0, (size_t)nwg * sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     void* args[] = {&a};
     return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);

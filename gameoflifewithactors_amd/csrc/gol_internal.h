@@ -77,8 +77,9 @@ int coop_k();
 int coop_m(int64_t nw);  // words per lane for rows of nw words (0: too wide for the pass)
 bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R);
 int64_t coop_xch_words(int64_t W, int nwg, int k);  // exchange buffer the pass needs
+// gens <= 65535 per launch; epoch (1..65535) tags this launch's hand-off granules (clear xch before reusing one)
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
-                            int64_t gens, bool bounded, unsigned* flags, int* err, uint32_t* xch, int64_t xch_words,
+                            int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
                             hipStream_t s);
 
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
