@@ -166,10 +166,12 @@ constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
-// Cooperative register-band pass (gol_coop.hip) for packed boards above the LDS-resident cut-over and up to
-// this many cells, up to 8192 wide: 512^2 0.87 vs 1.49 us/generation on the streaming pass, 2048^2 0.69 vs 1.48,
-// 4096^2 1.14 vs 1.62 (profiles/r2/small_coop_k.log).  GOL_COOP=0 disables it, GOL_COOP_MAX_CELLS moves the
-// cut-over (A/B runs; read per call).
+// Cooperative register-band pass (gol_coop.hip) for packed boards the single-wave pass does not take, up to this
+// many cells and 8192 wide: 4096^2 0.90 vs 1.62 us/generation on the streaming pass, 2048^2 0.46 vs 1.48, 512^2
+// 0.54 vs 1.49 (profiles/r2/ab_coop_granules_n.log); below the LDS-resident cut-over too: 256^2 bounded 0.44 vs
+// 0.92 on the LDS-resident pass, 512 x 256 0.54 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the
+// LDS-resident and streaming passes then take these boards), GOL_COOP_MAX_CELLS moves the upper cut-over (A/B
+// runs; read per call).
 constexpr int64_t kCoopMaxCells = (int64_t)1 << 25;
 bool coop_enabled() {
     const char* e = std::getenv("GOL_COOP");
@@ -384,25 +386,6 @@ int step_impl(gol_board* b, int64_t gens) {
         }
         return GOL_OK;
     }
-    if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
-        (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
-        const bool bounded = b->boundary == GOL_BOUNDED;
-        while (gens > 0) {
-            // one launch per 2^16 generations (a few tens of ms): a long gol_step stays interruptible by
-            // readbacks and other work on the board's stream
-            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
-            if (b->packed)
-                GOL_HIP(gol::launch_resident_packed(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, g,
-                                                    bounded, b->stream));
-            else
-                GOL_HIP(gol::launch_resident_bytes(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H, g, bounded,
-                                                   b->stream));
-            b->cur ^= 1;
-            b->generation += g;
-            gens -= g;
-        }
-        return GOL_OK;
-    }
     if (gens > 0 && use_coop(b)) {
         if (!b->coop) {
             GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
@@ -433,6 +416,25 @@ int step_impl(gol_board* b, int64_t gens) {
                                           b->boundary == GOL_BOUNDED, b->coop_epoch,
                                           reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
                                           b->coop_xch_words, b->stream));
+            b->cur ^= 1;
+            b->generation += g;
+            gens -= g;
+        }
+        return GOL_OK;
+    }
+    if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
+        (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
+        const bool bounded = b->boundary == GOL_BOUNDED;
+        while (gens > 0) {
+            // one launch per 2^16 generations (a few tens of ms): a long gol_step stays interruptible by
+            // readbacks and other work on the board's stream
+            const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
+            if (b->packed)
+                GOL_HIP(gol::launch_resident_packed(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, g,
+                                                    bounded, b->stream));
+            else
+                GOL_HIP(gol::launch_resident_bytes(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H, g, bounded,
+                                                   b->stream));
             b->cur ^= 1;
             b->generation += g;
             gens -= g;

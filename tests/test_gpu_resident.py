@@ -1,7 +1,7 @@
 """GPU parity of the LDS-resident small-board pass (csrc/gol_resident.hip).
 
-Boards up to 2^17 cells (packed ilv 1) or 2^14 cells (byte layout, widths not a multiple of 32) run a whole
-gol_step call as one launch with the board held in one workgroup's LDS by default; the kernel itself takes
+Boards up to 2^17 cells (packed ilv 1; with the cooperative pass off, GOL_COOP=0) or 2^14 cells (byte layout,
+widths not a multiple of 32) run a whole gol_step call as one launch with the board held in one workgroup's LDS; the kernel itself takes
 up to 2^19 / 2^16 cells, which these tests reach with GOL_RESIDENT_MAX_CELLS raised.  Bar: bit-exact against the oracle
 (GameOfLifeLogic.fs:56-63 rule, torus GameOfLifeDriver.fs:21-25, bounded Script.fsx:6-13) and against the
 streaming pass on the same board (GOL_RESIDENT_MAX_CELLS=0 forces the streaming pass; the C ABI reads the
@@ -29,9 +29,12 @@ def _rand(h, w, seed, p=0.5):
 
 
 def _run(gol, b0, boundary, steps, resident):
+    # the cooperative pass (taken first for packed boards by default) is off here: LDS-resident vs streaming
     h, w = b0.shape
-    old = os.environ.get("GOL_RESIDENT_MAX_CELLS")
+    keys = ("GOL_RESIDENT_MAX_CELLS", "GOL_COOP")
+    old = {k: os.environ.get(k) for k in keys}
     os.environ["GOL_RESIDENT_MAX_CELLS"] = str(1 << 20) if resident else "0"
+    os.environ["GOL_COOP"] = "0"
     try:
         with gol.Board(w, h, boundary) as b:
             b.set_cells(b0)
@@ -40,10 +43,11 @@ def _run(gol, b0, boundary, steps, resident):
             assert b.generation == sum(steps)
             return b.get_cells()
     finally:
-        if old is None:
-            os.environ.pop("GOL_RESIDENT_MAX_CELLS", None)
-        else:
-            os.environ["GOL_RESIDENT_MAX_CELLS"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 # (w, h): packed boards (w % 32 == 0) from one word per row to the 2^19-cell capacity, byte boards
