@@ -168,11 +168,11 @@ constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
 // Cooperative register-band pass (gol_coop.hip) for packed boards the single-wave pass does not take, up to this
 // many cells and 8192 wide: 4096^2 0.90 vs 1.62 us/generation on the streaming pass, 2048^2 0.46 vs 1.48, 512^2
-// 0.54 vs 1.49 (profiles/r2/ab_coop_granules_n.log); below the LDS-resident cut-over too: 256^2 bounded 0.44 vs
-// 0.92 on the LDS-resident pass, 512 x 256 0.54 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the
-// LDS-resident and streaming passes then take these boards), GOL_COOP_MAX_CELLS moves the upper cut-over (A/B
-// runs; read per call).
-constexpr int64_t kCoopMaxCells = (int64_t)1 << 25;
+// 0.54 vs 1.49 (profiles/r2/ab_coop_granules_n.log), 8192 x 4096 1.88 vs 2.95, 8192^2 2.24 vs 4.25, 4096 x 8192
+// 1.17 vs 4.14 (coop_wide_s.log); below the LDS-resident cut-over too: 256^2 bounded 0.44 vs 0.92 on the
+// LDS-resident pass, 512 x 256 0.54 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the LDS-resident and
+// streaming passes then take these boards), GOL_COOP_MAX_CELLS moves the upper cut-over (A/B runs; read per call).
+constexpr int64_t kCoopMaxCells = (int64_t)1 << 26;
 bool coop_enabled() {
     const char* e = std::getenv("GOL_COOP");
     return !(e && e[0] == '0');
@@ -184,13 +184,12 @@ constexpr int64_t kCoopMaxGensPerLaunch = 32768;  // a launch's granule tags cou
 // Layout and depth a new board gets when the caller leaves them at 0.
 int board_ilv(int64_t width, int64_t height) {
     const int env = pick_ilv(width);
-    if (std::getenv("GOL_ILV") == nullptr && width * height < kSmallBoardCells) {
-        // the cooperative pass sums interleaved blocks with 2 funnel shifts per block instead of 2 per word
-        const int m = width % 32 == 0 ? gol::coop_m(width / 32) : 0;
-        if (coop_enabled() && m > 1 && width * height > kResidentMaxCells) return m;
-        return 1;
-    }
-    return env;
+    if (std::getenv("GOL_ILV") != nullptr) return env;
+    const int64_t cells = width * height;
+    // boards the cooperative pass takes: its interleave, so a block costs 2 funnel shifts instead of 2 per word
+    const int m = width % 32 == 0 ? gol::coop_m(width / 32) : 0;
+    if (coop_enabled() && m > 1 && cells > kResidentMaxCells && cells <= kCoopMaxCells) return m;
+    return cells < kSmallBoardCells ? 1 : env;
 }
 // Boards up to this many cells run every gol_step call as ONE launch of the LDS-resident kernel
 // (gol_resident.hip) when the layout fits it: whole board in one workgroup's LDS, one barrier per
