@@ -167,10 +167,10 @@ constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
 // Cooperative register-band pass (gol_coop.hip) for packed boards the single-wave pass does not take, up to this
-// many cells and 8192 wide: 4096^2 0.90 vs 1.62 us/generation on the streaming pass, 2048^2 0.46 vs 1.48, 512^2
-// 0.54 vs 1.49 (profiles/r2/ab_coop_granules_n.log), 8192 x 4096 1.88 vs 2.95, 8192^2 2.24 vs 4.25, 4096 x 8192
-// 1.17 vs 4.14 (coop_wide_s.log); below the LDS-resident cut-over too: 256^2 bounded 0.44 vs 0.92 on the
-// LDS-resident pass, 512 x 256 0.54 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the LDS-resident and
+// many cells and 8192 wide: 4096^2 0.81 vs 1.62 us/generation on the streaming pass, 2048^2 0.44 vs 1.48, 512^2
+// 0.50 vs 1.49 (profiles/r2/ab_coop_xh_u.log), 8192 x 4096 1.76 vs 2.95, 8192^2 2.16 vs 4.25, 4096 x 8192 1.01
+// vs 4.14 (coop_wide_u.log, coop_wide_s.log); below the LDS-resident cut-over too: 256^2 bounded 0.41 vs 0.92 on
+// the LDS-resident pass, 512 x 256 0.50 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the LDS-resident and
 // streaming passes then take these boards), GOL_COOP_MAX_CELLS moves the upper cut-over (A/B runs; read per call).
 constexpr int64_t kCoopMaxCells = (int64_t)1 << 26;
 bool coop_enabled() {

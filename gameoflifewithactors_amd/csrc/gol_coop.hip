@@ -38,6 +38,11 @@ constexpr int kWaves = 16;                 // waves per workgroup: 4 per SIMD
 constexpr int kThreads = 64 * kWaves;
 constexpr int kMinLds = 96 * 1024;         // > half the CU's 160 KiB: one workgroup per CU
 constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident
+// The wave-edge exchange per generation carries the edge rows' horizontal sums (1) or the raw rows (0, A/B)
+#ifndef GOL_COOP_XH
+#define GOL_COOP_XH 1
+#endif
+constexpr int kSlotRows = GOL_COOP_XH ? 4 : 2;  // LDS words per lane and word of a row, per wave and parity
 
 
 struct CoopArgs {
@@ -183,15 +188,38 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         for (int j = 0; j < k; j++) {
             const int gen = blk * K + j;  // generation of this launch
             const int par = gen & 1;      // alternates across blocks too: no barrier separates them
-            uint32_t* slot = xs + (par * kWaves) * 2 * M * 64;
+            uint32_t* slot = xs + (par * kWaves) * kSlotRows * M * 64;
+            const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
+            const bool active = r0 < hi && r0 + R > lo;  // wave-uniform: some of this wave's rows are produced
+            uint32_t so[R][M], co[R][M];
+#if GOL_COOP_XH
+            // every wave publishes the row sums of its first and last rows (inactive waves too: their rows border
+            // active ones), so no wave re-sums a neighbour's row
+#pragma unroll
+            for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+#pragma unroll
+            for (int t = 0; t < M; t++) {
+                slot[((wv * 4 + 0) * M + t) * 64 + lane] = so[0][t];
+                slot[((wv * 4 + 1) * M + t) * 64 + lane] = co[0][t];
+                slot[((wv * 4 + 2) * M + t) * 64 + lane] = so[R - 1][t];
+                slot[((wv * 4 + 3) * M + t) * 64 + lane] = co[R - 1][t];
+            }
+            __syncthreads();
+            if (!active) continue;
+            uint32_t sa[M], ca[M], sb[M], cb[M];
+#pragma unroll
+            for (int t = 0; t < M; t++) {
+                sa[t] = wv > 0 ? slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane] : 0u;
+                ca[t] = wv > 0 ? slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane] : 0u;
+                sb[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane] : 0u;
+                cb[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 4 + 1) * M + t) * 64 + lane] : 0u;
+            }
+#else
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 slot[((wv * 2 + 0) * M + t) * 64 + lane] = w[0][t];
                 slot[((wv * 2 + 1) * M + t) * 64 + lane] = w[R - 1][t];
             }
-            const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
-            const bool active = r0 < hi && r0 + R > lo;  // wave-uniform: some of this wave's rows are produced
-            uint32_t so[R][M], co[R][M];
             if (active) {
 #pragma unroll
                 for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
@@ -207,6 +235,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             uint32_t sa[M], ca[M], sb[M], cb[M];
             lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sa, ca);
             lane_row_sum<M, ILV, BOUNDED, FULL>(below, lane, nl, sb, cb);
+#endif
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const bool dead = BOUNDED && !on_board(gy_of(r0 + i));  // dead outside the board at every generation
@@ -364,7 +393,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     const void* fn = M == 1 ? kernel_m<1>(R, false, bounded, full)
                             : (M == 2 ? kernel_m<2>(R, il, bounded, full) : kernel_m<4>(R, il, bounded, full));
     if (!fn) return hipErrorInvalidValue;
-    const size_t need = (size_t)2 * kWaves * 2 * M * 64 * 4;
+    const size_t need = (size_t)2 * kWaves * kSlotRows * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
