@@ -404,6 +404,9 @@ int step_impl(gol_board* b, int64_t gens) {
             GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
             b->coop_xch_words = need;
             b->coop_epoch = 0xffff;  // forces the clear below: a fresh buffer holds arbitrary tags
+        } else if (const char* e0 = std::getenv("GOL_COOP_EPOCH")) {
+            // tests: the next launch's epoch (runs the 16-bit wrap, and the clear of the granules it needs, early)
+            b->coop_epoch = (unsigned)std::atoi(e0) & 0xffffu;
         }
         while (gens > 0) {
             const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;

@@ -29,7 +29,10 @@
 #include "gol_internal.h"
 #include "gol_bitlogic.h"
 
+#include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 namespace gol {
 namespace {
@@ -395,8 +398,16 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     if (!fn) return hipErrorInvalidValue;
     const size_t need = (size_t)2 * kWaves * kSlotRows * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    {  // the LDS attribute once per kernel (a host call per launch otherwise)
+        static std::mutex mu;
+        static std::vector<const void*> done;
+        std::lock_guard<std::mutex> lock(mu);
+        if (std::find(done.begin(), done.end(), fn) == done.end()) {
+            const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            done.push_back(fn);
+        }
+    }
     void* args[] = {&a};
     return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);
 }

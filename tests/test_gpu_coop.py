@@ -104,3 +104,21 @@ def test_coop_config2_golden_checkpoints(gol):
             b.step(gen - done)
             done = gen
             assert (b.hash(), b.population()) == (h, pop), gen
+
+
+def test_coop_epoch_wrap(gol, oracle):
+    """The hand-off granules carry a 16-bit launch epoch; at the wrap the host clears them. Launches just before,
+    at and after the wrap (GOL_COOP_EPOCH sets the epoch of the last launch) must stay exact."""
+    b0 = _rand(1024, 1024, 77)
+    with _Env(GOL_COOP="1"), gol.Board(1024, 1024, 0) as b:
+        b.set_cells(b0)
+        b.step(9)  # first launch: allocates and clears the exchange buffer
+        done = 9
+        for epoch in (0xfffd, 0xfffe, 0xffff):
+            with _Env(GOL_COOP_EPOCH=str(epoch)):
+                b.step(17)  # this launch runs at epoch + 1 (the last one wraps to 1 and clears)
+            done += 17
+        b.step(17)
+        done += 17
+        np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, done, 0))
+
