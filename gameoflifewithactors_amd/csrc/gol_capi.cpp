@@ -996,7 +996,7 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     if (seg_rows) *seg_rows = a.seg;
     if (waves)
         *waves = a.nstrips * a.nsegs *
-                 (a.split > 0 ? gol::stream_wpb(k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
+                 (a.split > 0 ? gol::stream_wpb(a.words, k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
     return GOL_OK;
 }
 

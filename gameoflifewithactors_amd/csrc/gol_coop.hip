@@ -46,6 +46,9 @@ constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a ba
 #define GOL_COOP_XH 1
 #endif
 constexpr int kSlotRows = GOL_COOP_XH ? 4 : 2;  // LDS words per lane and word of a row, per wave and parity
+// LDS slots per parity: one per wave, plus a zero slot on each side (the neighbours of the first and last
+// waves), so every wave reads its neighbours' slots without a branch
+constexpr int kSlots = kWaves + 2;
 
 
 struct CoopArgs {
@@ -131,7 +134,7 @@ __device__ __forceinline__ void lane_row_sum(const uint32_t (&r)[M], int lane, i
 
 template <int M, int R, bool ILV, bool BOUNDED, bool FULL>
 __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
-    extern __shared__ uint32_t xs[];  // [2 parity][kWaves][2 (first row, last row)][M][64 lanes], then kWaves counters
+    extern __shared__ uint32_t xs[];  // [2 parity][kSlots][kSlotRows][M][64 lanes]; slots 0 and kSlots - 1 stay zero
     const int band = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -168,6 +171,14 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         }
     }
 
+    if (wv == 0 || wv == kWaves - 1) {  // the zero slots beside the first and last waves (both parities)
+        const int z = wv == 0 ? 0 : kSlots - 1;
+#pragma unroll
+        for (int par = 0; par < 2; par++)
+#pragma unroll
+            for (int t = 0; t < kSlotRows * M; t++) xs[((par * kSlots + z) * kSlotRows * M + t) * 64 + lane] = 0u;
+    }  // ordered before their first read by the first generation's barrier
+
     const int nblk = (a.gens + K - 1) / K;
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
@@ -191,7 +202,8 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         for (int j = 0; j < k; j++) {
             const int gen = blk * K + j;  // generation of this launch
             const int par = gen & 1;      // alternates across blocks too: no barrier separates them
-            uint32_t* slot = xs + (par * kWaves) * kSlotRows * M * 64;
+            uint32_t* slot = xs + (par * kSlots + 1) * kSlotRows * M * 64;  // slot[-1] and slot[kWaves] are zero
+            // (dead outside a bounded board at every generation: `dead` below)
             const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
             const bool active = r0 < hi && r0 + R > lo;  // wave-uniform: some of this wave's rows are produced
             uint32_t so[R][M], co[R][M];
@@ -207,15 +219,41 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                 slot[((wv * 4 + 2) * M + t) * 64 + lane] = so[R - 1][t];
                 slot[((wv * 4 + 3) * M + t) * 64 + lane] = co[R - 1][t];
             }
+            // the wave's interior rows need no neighbour: stepped while the edge sums travel through LDS
+            if (active) {
+#pragma unroll
+                for (int i = 1; i + 1 < R; i++) {
+                    const bool dead = BOUNDED && !on_board(gy_of(r0 + i));
+#pragma unroll
+                    for (int t = 0; t < M; t++) {
+                        const uint32_t v = life_next(so[i - 1][t], co[i - 1][t], so[i][t], co[i][t], so[i + 1][t],
+                                                     co[i + 1][t], w[i][t]);
+                        w[i][t] = dead || !lane_on ? 0u : v;
+                    }
+                }
+            }
             __syncthreads();
             if (!active) continue;
             uint32_t sa[M], ca[M], sb[M], cb[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
-                sa[t] = wv > 0 ? slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane] : 0u;
-                ca[t] = wv > 0 ? slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane] : 0u;
-                sb[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane] : 0u;
-                cb[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 4 + 1) * M + t) * 64 + lane] : 0u;
+                sa[t] = slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane];
+                ca[t] = slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane];
+                sb[t] = slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane];
+                cb[t] = slot[(((wv + 1) * 4 + 1) * M + t) * 64 + lane];
+            }
+            constexpr int kEdgeRows = R > 1 ? 2 : 1;  // rows 0 and R - 1 (interior rows are done)
+#pragma unroll
+            for (int e = 0; e < kEdgeRows; e++) {
+                const int i = e == 0 ? 0 : R - 1;
+                const bool dead = BOUNDED && !on_board(gy_of(r0 + i));
+#pragma unroll
+                for (int t = 0; t < M; t++) {
+                    const uint32_t v = life_next(i == 0 ? sa[t] : so[i - 1][t], i == 0 ? ca[t] : co[i - 1][t], so[i][t],
+                                                 co[i][t], i == R - 1 ? sb[t] : so[i + 1][t],
+                                                 i == R - 1 ? cb[t] : co[i + 1][t], w[i][t]);
+                    w[i][t] = dead || !lane_on ? 0u : v;
+                }
             }
 #else
 #pragma unroll
@@ -232,13 +270,12 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             uint32_t above[M], below[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
-                above[t] = wv > 0 ? slot[(((wv - 1) * 2 + 1) * M + t) * 64 + lane] : 0u;
-                below[t] = wv + 1 < kWaves ? slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane] : 0u;
+                above[t] = slot[(((wv - 1) * 2 + 1) * M + t) * 64 + lane];
+                below[t] = slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane];
             }
             uint32_t sa[M], ca[M], sb[M], cb[M];
             lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sa, ca);
             lane_row_sum<M, ILV, BOUNDED, FULL>(below, lane, nl, sb, cb);
-#endif
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const bool dead = BOUNDED && !on_board(gy_of(r0 + i));  // dead outside the board at every generation
@@ -250,6 +287,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     w[i][t] = dead || !lane_on ? 0u : v;
                 }
             }
+#endif
         }
         if (blk + 1 == nblk) break;
         // ---- hand-off: the band's first and last K rows as granules of parity blk & 1
@@ -396,7 +434,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     const void* fn = M == 1 ? kernel_m<1>(R, false, bounded, full)
                             : (M == 2 ? kernel_m<2>(R, il, bounded, full) : kernel_m<4>(R, il, bounded, full));
     if (!fn) return hipErrorInvalidValue;
-    const size_t need = (size_t)2 * kWaves * kSlotRows * M * 64 * 4;
+    const size_t need = (size_t)2 * kSlots * kSlotRows * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
     {  // the LDS attribute once per kernel (a host call per launch otherwise)
         static std::mutex mu;

@@ -30,7 +30,7 @@ int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 int64_t stream_strips(int64_t words, int ilv, int k, bool bounded);
 int stream_pair_split(int k, int ilv, bool bounded);
-int stream_wpb(int k, int ilv, bool bounded, bool wrap);
+int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,

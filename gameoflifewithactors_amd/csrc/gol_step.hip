@@ -41,15 +41,14 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 // Waves per workgroup of a variant: 4 x the waves each SIMD holds at the kernel's register footprint, so
 // ONE workgroup fills a CU and the waves sharing a SIMD (w, w + 4, w + 8) belong to the same workgroup
 // (their age order is then known: see the group split in plan_stream).  (K, M) = (12, 2) runs 12-wave
-// workgroups at 3 waves/SIMD (168 VGPRs; profiles/r1/w12_sweep*.log) in both torus variants.  The bounded
-// variant carries row/column masks and spills at that budget (profiles/r1/strip_bounded_sweep.log: bounded
-// K = 12 41k GCUPS with 12-wave workgroups, 74k with 8), so it keeps 8.
-#ifndef GOL_BOUNDED_W12
-#define GOL_BOUNDED_W12 0
-#endif
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+// workgroups at 3 waves/SIMD (168 VGPRs; profiles/r1/w12_sweep*.log) in both torus variants and on bounded
+// boards at least a strip wide (edge-fill strips: row masks only, 164 VGPRs).  The NARROW bounded variant (a
+// board narrower than one strip) also carries per-lane column masks, which spill at that budget (185 VGPRs;
+// round 1 measured 41k GCUPS with 12-wave workgroups, 74k with 8, profiles/r1/strip_bounded_sweep.log), so it
+// keeps 8.
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
 struct Wpb {
-    static constexpr int value = (GOL_BOUNDED_W12 || !BOUNDED) && K == 12 && M == 2 ? 12 : kWavesPerBlock;
+    static constexpr int value = !NARROW && K == 12 && M == 2 ? 12 : kWavesPerBlock;
 };
 
 // Block-edge words of the neighbouring lanes, by DPP (a half-rate VALU move on gfx950,
@@ -148,7 +147,10 @@ struct TripRows {
 };
 
 // One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+// NARROW (bounded only): the board is narrower than one wave strip, so lanes can lie off the board and every
+// level masks columns as well as rows.  Bounded boards at least a strip wide use edge-fill strips (no lane off
+// the board) and mask rows only: the column mask and its register are compiled out.
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
 struct StreamWave {
     static constexpr int R = TripRows<K, M>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
@@ -160,13 +162,17 @@ struct StreamWave {
     // (profiles/r1/k1_nohalo_ab.log: 3.9-4.1 -> 4.7-5.1 TB/s).
     static constexpr bool kNoHalo = K == 1;
     static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
+    // per-lane column masks: narrow bounded boards, and the K = 1 halo-free strips (their last strip may end
+    // past the board's last block)
+    static constexpr bool kColMask = BOUNDED && (NARROW || kNoHalo);
+    static_assert(BOUNDED || !NARROW, "NARROW is a bounded-board variant");
 
     const uint32_t* __restrict__ src;
     uint32_t* __restrict__ dst;
     const StreamArgs& a;
     int load_off;      // this lane's byte offset in a row (its block column)
     int store_off;     // = load_off for interior on-board lanes, kNoStore otherwise
-    uint32_t colmask;  // bounded: ~0 for an on-board block
+    uint32_t colmask;  // kColMask: ~0 for an on-board block
     int64_t row_bytes;
     int64_t seg_begin, seg_end, nsteps, ly0;
     int64_t load_br;  // wrap: buffer row of the next level-0 row to load; else buffer row of step 0 (uniform)
@@ -191,7 +197,7 @@ struct StreamWave {
     // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
     // of a pair), applied to each wave's streamed rows (its share plus the 2K-row pipeline fill).
     __device__ __forceinline__ int64_t group_cut(int64_t len, int i) const {
-        constexpr int n = Wpb<K, M, BOUNDED, WRAP_ROWS>::value / 4;
+        constexpr int n = Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value / 4;
         if (i <= 0) return 0;
         if (i >= n) return len;
         const float f = (float)a.split * (1.0f / 65536.0f);
@@ -219,9 +225,9 @@ struct StreamWave {
         // no column mask at any level.  Interior strips overlap by two blocks as on a torus (halo lanes).
         // this lane's block column (may be off-board)
         int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
-        if constexpr (BOUNDED && !kNoHalo) {
-            edge_fill = nblocks >= kWave;
-            if (edge_fill) cb = (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane;
+        if constexpr (BOUNDED && !kNoHalo && !NARROW) {  // the host picks NARROW exactly when nblocks < kWave
+            edge_fill = true;
+            cb = (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane;
         }
         int64_t lc;
         if (BOUNDED) {
@@ -329,7 +335,7 @@ struct StreamWave {
             if (BOUNDED) {
                 const uint32_t rm = row_mask((int)first_step + r);
 #pragma unroll
-                for (int j = 0; j < M; j++) buf[r][j] = lut3<0x80>(buf[r][j], colmask, rm);  // a & b & c
+                for (int j = 0; j < M; j++) buf[r][j] = kColMask ? lut3<0x80>(buf[r][j], colmask, rm) : buf[r][j] & rm;
                 if (kNoHalo) nb[r] = lut3<0x80>(nb[r], nbmask, rm);
             }
         }
@@ -354,7 +360,7 @@ struct StreamWave {
 #pragma unroll
         for (int j = 0; j < M; j++) {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
-            if (BOUNDED && MASK) out[j] = lut3<0x80>(out[j], colmask, rowmask);  // dead off the board
+            if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask, rowmask) : out[j] & rowmask;  // dead off the board
             sP[j] = sN[j];
             cP[j] = cN[j];
         }
@@ -455,25 +461,26 @@ struct StreamWave {
 };
 
 // Minimum waves per SIMD the register allocator must fit (1 = compiler's choice), per variant.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
 struct MinWaves {
-    static constexpr int value = Wpb<K, M, BOUNDED, WRAP_ROWS>::value > 8 ? Wpb<K, M, BOUNDED, WRAP_ROWS>::value / 4 : 1;
+    static constexpr int value =
+        Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value > 8 ? Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value / 4 : 1;
 };
 
 // Wave strips: Wpb waves per workgroup, each its own column strip and segment (or a share of a group
 // segment, see plan_stream).
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS>
-__global__ __launch_bounds__((kWave * Wpb<K, M, BOUNDED, WRAP_ROWS>::value))
-__attribute__((amdgpu_waves_per_eu(MinWaves<K, M, BOUNDED, WRAP_ROWS>::value)))
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
+__global__ __launch_bounds__((kWave * Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value))
+__attribute__((amdgpu_waves_per_eu(MinWaves<K, M, BOUNDED, WRAP_ROWS, NARROW>::value)))
 void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
-    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS>;
+    using W = StreamWave<K, M, BOUNDED, WRAP_ROWS, NARROW>;
     constexpr int R = W::R;
     const int lane = threadIdx.x & (kWave - 1);
     int64_t sx, sy;
     int role = -1;
     // wave index made provably uniform so all row bookkeeping lives in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS>::value;
+    constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value;
     if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
         const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
         role = wave >> 2;  // 0 = the oldest
@@ -613,17 +620,25 @@ int stream_largest_k(int64_t n, int cap, int ilv) {
     return 1;
 }
 
-// Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
-// (never wraps: rows beyond the board are masked dead).
-template <int K, int M>
-static const void* stream_kernel(bool bounded, bool wrap) {
-    if (bounded) return (const void*)&gol_stream_step<K, M, true, false>;
-    return wrap ? (const void*)&gol_stream_step<K, M, false, true> : (const void*)&gol_stream_step<K, M, false, false>;
+// A bounded board narrower than one wave strip takes the column-masked variant (StreamWave NARROW).
+static bool stream_narrow(int64_t words, int ilv, int k, bool bounded) {
+    return bounded && k > 1 && words / ilv < kWave;
 }
 
-static const void* kernel_for(int k, int ilv, bool bounded, bool wrap) {
+// Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
+// (never wraps: rows beyond the board are masked dead; narrow boards mask columns too).
+template <int K, int M>
+static const void* stream_kernel(bool bounded, bool wrap, bool narrow) {
+    if (bounded)
+        return narrow ? (const void*)&gol_stream_step<K, M, true, false, true>
+                      : (const void*)&gol_stream_step<K, M, true, false, false>;
+    return wrap ? (const void*)&gol_stream_step<K, M, false, true, false>
+                : (const void*)&gol_stream_step<K, M, false, false, false>;
+}
+
+static const void* kernel_for(int k, int ilv, bool bounded, bool wrap, bool narrow) {
 #define GOL_KPTR(K_, M_) \
-    if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap);
+    if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap, narrow);
     GOL_FOR_EACH_KM(GOL_KPTR)
 #undef GOL_KPTR
     return nullptr;
@@ -639,10 +654,12 @@ int64_t stream_strips(int64_t words, int ilv, int k, bool bounded) {
 }
 
 // Waves per workgroup of a variant (Wpb)
-int stream_wpb(int k, int ilv, bool bounded, bool wrap) {
-    if (bounded) return kWavesPerBlock;
-#define GOL_WPBQ(K_, M_) \
-    if (k == K_ && ilv == M_) return wrap ? Wpb<K_, M_, false, true>::value : Wpb<K_, M_, false, false>::value;
+int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap) {
+    const bool narrow = stream_narrow(words, ilv, k, bounded);
+#define GOL_WPBQ(K_, M_)                                                                                 \
+    if (k == K_ && ilv == M_)                                                                            \
+        return bounded ? (narrow ? Wpb<K_, M_, true, false, true>::value : Wpb<K_, M_, true, false, false>::value) \
+                       : (wrap ? Wpb<K_, M_, false, true, false>::value : Wpb<K_, M_, false, false, false>::value);
     GOL_FOR_EACH_KM(GOL_WPBQ)
 #undef GOL_WPBQ
     return kWavesPerBlock;
@@ -675,15 +692,16 @@ int stream_pair_split(int k, int ilv, bool bounded) {
 
 // Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.  Falls back
 // to 4096 waves when no device answers (host-only planning, e.g. CPU tests).
-static int64_t resident_units(int k, int ilv, bool bounded, bool wrap) {
-    static std::atomic<int64_t> cache[33][5][2][2];
+static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool wrap) {
+    static std::atomic<int64_t> cache[33][5][2][2][2];
     const int64_t fallback = 4096;
     if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return fallback;
     if (bounded) wrap = false;
-    int64_t v = cache[k][ilv][bounded][wrap].load(std::memory_order_relaxed);
+    const bool narrow = stream_narrow(words, ilv, k, bounded);
+    int64_t v = cache[k][ilv][bounded][wrap][narrow].load(std::memory_order_relaxed);
     if (v > 0) return v;
-    const void* fn = kernel_for(k, ilv, bounded, wrap);
-    const int wpb = stream_wpb(k, ilv, bounded, wrap);
+    const void* fn = kernel_for(k, ilv, bounded, wrap, narrow);
+    const int wpb = stream_wpb(words, k, ilv, bounded, wrap);
     const int threads = kWave * wpb;
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
@@ -694,7 +712,7 @@ static int64_t resident_units(int k, int ilv, bool bounded, bool wrap) {
         return fallback;
     }
     v = (int64_t)blocks * cus * wpb;
-    cache[k][ilv][bounded][wrap].store(v, std::memory_order_relaxed);
+    cache[k][ilv][bounded][wrap][narrow].store(v, std::memory_order_relaxed);
     return v;
 }
 
@@ -717,12 +735,12 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     // a launch too short for one full group segment per strip (e.g. a k-row halo band) runs one wave per
     // segment: splitting a handful of rows only multiplies the pipeline fill
-    const int wpb = stream_wpb(k, a.ilv, bounded, wrap);
+    const int wpb = stream_wpb(a.words, k, a.ilv, bounded, wrap);
     if (a.split && rows < (int64_t)(wpb / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
     int64_t seg = env_seg;
     if (seg <= 0) {
         const int group = a.split ? wpb / 4 : 1;  // waves per segment
-        int64_t units = resident_units(k, a.ilv, bounded, wrap);
+        int64_t units = resident_units(a.words, k, a.ilv, bounded, wrap);
         if (a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
         const int64_t slots = units / group;
         int64_t nsegs = slots / a.nstrips;
@@ -745,17 +763,20 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
 template <int K, int M>
 static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
                             hipStream_t s) {
-    const int WPB = stream_wpb(K, M, bounded, wrap);
+    const int WPB = stream_wpb(a.words, K, M, bounded, wrap);
     const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
     const unsigned blocks = (unsigned)((waves + WPB - 1) / WPB);
     const dim3 block(kWave * WPB);
     if (bounded) {
-        hipLaunchKernelGGL((gol_stream_step<K, M, true, false>), dim3(blocks), block, 0, s, src, dst, a);
+        if (stream_narrow(a.words, M, K, true))
+            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, true>), dim3(blocks), block, 0, s, src, dst, a);
+        else
+            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, false>), dim3(blocks), block, 0, s, src, dst, a);
     } else {
         if (wrap)
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, true>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, true, false>), dim3(blocks), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, false, false>), dim3(blocks), block, 0, s, src, dst, a);
     }
     return hipGetLastError();
 }

@@ -389,16 +389,40 @@ def test_native_host_mirror_driver():
 # ---------------------------------------------------------------- bounded boards: edge-fill strips
 @pytest.mark.parametrize("ilv", [1, 2])
 @pytest.mark.parametrize("nblocks", [64, 65, 124, 125, 126, 127, 189, 1024])
-def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks):
+def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks, monkeypatch):
     """Bounded boards at least a strip (64 blocks) wide place their first strip at the board's left edge and
     the last at its right edge (the dead cells beyond the edges arrive as the DPP moves' zero fill), and run
-    only the trips that produce rows off the board masked (Script.fsx:6-13).  Every strip-count boundary
-    (nblocks around multiples of 62), the top/bottom trips of the first/last segments, a deep block and a
-    remainder pass, against the oracle."""
+    only the trips that produce rows off the board masked (Script.fsx:6-13), in the variant without column
+    masks (12-wave workgroups at K = 12).  Every strip-count boundary (nblocks around multiples of 62), the
+    top/bottom trips of the first/last segments, a deep block and a remainder pass, against the oracle.  The
+    cooperative pass is switched off so the streaming kernel runs every width."""
+    monkeypatch.setenv("GOL_COOP", "0")
     w = 32 * ilv * nblocks
     h = 300 if nblocks < 1024 else 64
     b0 = _rand(h, w, nblocks * 10 + ilv, p=0.4)
     for k in (16, 12, 8):
         with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv) as b:
+            assert b.info()["tblock_k"] == k
+            b.set_cells(b0).step(2 * k + 5)
+            np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 2 * k + 5, 1), err_msg=f"k={k}")
+
+
+@pytest.mark.parametrize("ilv", [1, 2])
+@pytest.mark.parametrize("nblocks", [1, 2, 31, 62, 63])
+def test_bounded_narrow_strips_match_oracle(gol, oracle, ilv, nblocks, monkeypatch):
+    """Bounded boards narrower than one strip (< 64 blocks) take the NARROW streaming variant: lanes off the
+    board, column masks at every level (Script.fsx:6-13).  The single-wave, cooperative and LDS-resident
+    passes are switched off so the streaming kernel runs, at deep, mid and remainder depths."""
+    for key in ("GOL_COOP", "GOL_WAVE_RESIDENT", "GOL_RESIDENT_MAX_CELLS"):
+        monkeypatch.setenv(key, "0")
+    w = 32 * ilv * nblocks
+    h = 150
+    if w < 3:
+        pytest.skip("board narrower than 3 cells")
+    b0 = _rand(h, w, nblocks * 7 + ilv, p=0.4)
+    for k in (16, 12, 8):
+        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv) as b:
+            if b.info()["tblock_k"] != k:
+                continue  # depth not supported at this layout
             b.set_cells(b0).step(2 * k + 5)
             np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 2 * k + 5, 1), err_msg=f"k={k}")
