@@ -45,6 +45,11 @@ constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a ba
 #ifndef GOL_COOP_XH
 #define GOL_COOP_XH 1
 #endif
+// Diagnostic builds only (wrong results by design, timing decomposition): 1 no per-generation barrier, 2 no LDS
+// reads, 3 no LDS traffic (barrier kept), 4 no hand-off between bands
+#ifndef GOL_COOP_DEBUG
+#define GOL_COOP_DEBUG 0
+#endif
 constexpr int kSlotRows = GOL_COOP_XH ? 4 : 2;  // LDS words per lane and word of a row, per wave and parity
 // LDS slots per parity: one per wave, plus a zero slot on each side (the neighbours of the first and last
 // waves), so every wave reads its neighbours' slots without a branch
@@ -63,6 +68,7 @@ struct CoopArgs {
     int K;                // generations per block (<= every band's height)
     int gens;
     unsigned epoch;       // launch epoch (16 bits) of the granule tags
+    int poll_delay;       // s_sleep 1 periods (64 clocks) before the first poll of a hand-off
     int* err;             // set to 1 by a timed-out wait
 };
 
@@ -73,24 +79,62 @@ __device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M],
     for (int t = 0; t < M; t++)
         __hip_atomic_store(p + t, (uint64_t)tag << 32 | w[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// ... and back: poll each granule (8-byte sc1 loads) until its tag matches; false after the spin limit
-template <int M>
-__device__ __forceinline__ bool ld_granules(const uint64_t* p, uint32_t (&w)[M], unsigned tag) {
-    bool ok = true;
+// ... and back, false after the spin limit.  The hand-off is latency-bound: at 4096^2 it costs ~2 us per block
+// of 8 generations, 0.25 of the 0.72 us per generation (profiles/r2/coop_decomp_y.log: the pass without it).
+// The neighbour publishes at about the time this band starts polling, so a poll issued at once often returns
+// before the data is visible and costs a second memory round trip.  Rows of up to 128 words (M <= 2): every
+// granule the wave needs (R rows x M words per lane) in ONE batch of 8-byte sc1 loads per poll round, after a
+// short delay (`delay` s_sleep 1 periods, 8 by default: ~250 ns); 4096^2 0.70 vs 0.72 us/generation, bounded
+// 0.68 vs 0.74, 2048^2 0.41 vs 0.44 (profiles/r2/coop_delay_za.log).  Wider rows (M = 4: 8 granules per lane and
+// row pair) ran slower batched (8192 x 4096 1.69 vs 1.61) and poll granule by granule, at once.
+template <int M, int R>
+__device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uint32_t (&w)[R][M], unsigned tag,
+                                            int delay) {
+    if constexpr (M >= 4) {
+        bool ok = true;
 #pragma unroll
-    for (int t = 0; t < M; t++) {
-        uint64_t v = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (unsigned i = 0; (unsigned)(v >> 32) != tag; i++) {
-            if (i == kSpinLimit) {
-                ok = false;
-                break;
+        for (int i = 0; i < R; i++) {
+            if (!src[i]) continue;
+#pragma unroll
+            for (int t = 0; t < M; t++) {
+                uint64_t g = __hip_atomic_load(src[i] + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (unsigned it = 0; (unsigned)(g >> 32) != tag; it++) {
+                    if (it == kSpinLimit) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    g = __hip_atomic_load(src[i] + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                w[i][t] = (uint32_t)g;
             }
-            __builtin_amdgcn_s_sleep(1);
-            v = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        w[t] = (uint32_t)v;
+        return ok;
     }
-    return ok;
+    for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
+    uint64_t v[R][M];
+    for (unsigned it = 0;; it++) {
+#pragma unroll
+        for (int i = 0; i < R; i++)
+#pragma unroll
+            for (int t = 0; t < M; t++)
+                v[i][t] = src[i] ? __hip_atomic_load(src[i] + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (uint64_t)tag << 32;
+        bool miss = false;
+#pragma unroll
+        for (int i = 0; i < R; i++)
+#pragma unroll
+            for (int t = 0; t < M; t++) miss = miss || (unsigned)(v[i][t] >> 32) != tag;
+        if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
+        if (it == kSpinLimit) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+        if (src[i])
+#pragma unroll
+            for (int t = 0; t < M; t++) w[i][t] = (uint32_t)v[i][t];
+    return true;
 }
 
 // Word of the lane to the left / right.  FULL (all 64 lanes hold words): DPP rotate on a torus, DPP shift with
@@ -171,6 +215,11 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         }
     }
 
+    // The band's initial rows must have arrived before the generation loop: a wait left for the compiler lands
+    // INSIDE the loop (first use), and there s_waitcnt vmcnt(0) also waits for the hand-off's write-through
+    // stores (vmcnt counts stores): every producer wave then stalled for its stores' completion in the first
+    // generation of every block.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     if (wv == 0 || wv == kWaves - 1) {  // the zero slots beside the first and last waves (both parities)
         const int z = wv == 0 ? 0 : kSlots - 1;
 #pragma unroll
@@ -182,19 +231,23 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     const int nblk = (a.gens + K - 1) / K;
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
-        if (blk > 0) {
+        if (blk > 0 && GOL_COOP_DEBUG != 4) {
             // halo rows: the neighbours' edge rows of block blk - 1 (parity (blk - 1) & 1), polled granule by granule
             const int par = (blk - 1) & 1;
-            bool ok = true;
+            const uint64_t* src[R];
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const int li = r0 + i;
-                const uint64_t* src = nullptr;
-                if (li < K && up >= 0) src = xrow(par, up, 1, li);                              // up band's bottom rows
-                else if (li >= K + B && li < L && dn >= 0) src = xrow(par, dn, 0, li - K - B);  // dn band's top rows
-                if (src && lane_on) ok = ld_granules<M>(src + col, w[i], tag_of(blk - 1)) && ok;
+                src[i] = nullptr;
+                if (!lane_on) continue;
+                if (li < K && up >= 0) src[i] = xrow(par, up, 1, li) + col;                              // up band's bottom rows
+                else if (li >= K + B && li < L && dn >= 0) src[i] = xrow(par, dn, 0, li - K - B) + col;  // dn band's top rows
             }
-            if (!ok) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool any = false;
+#pragma unroll
+            for (int i = 0; i < R; i++) any = any || src[i] != nullptr;
+            if (__builtin_amdgcn_ballot_w64(any) != 0 && !ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay))
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j).  The wave's own row
         // sums do not depend on the exchange: they are summed between publishing the edge rows and the barrier,
@@ -213,7 +266,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
 #pragma unroll
             for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
 #pragma unroll
-            for (int t = 0; t < M; t++) {
+            for (int t = 0; t < M && GOL_COOP_DEBUG != 3; t++) {
                 slot[((wv * 4 + 0) * M + t) * 64 + lane] = so[0][t];
                 slot[((wv * 4 + 1) * M + t) * 64 + lane] = co[0][t];
                 slot[((wv * 4 + 2) * M + t) * 64 + lane] = so[R - 1][t];
@@ -232,11 +285,18 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     }
                 }
             }
-            __syncthreads();
+            if (GOL_COOP_DEBUG != 1) __syncthreads();
             if (!active) continue;
             uint32_t sa[M], ca[M], sb[M], cb[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
+                if (GOL_COOP_DEBUG == 2 || GOL_COOP_DEBUG == 3) {
+                    sa[t] = so[0][t] ^ (uint32_t)j;
+                    ca[t] = co[0][t];
+                    sb[t] = so[R - 1][t];
+                    cb[t] = co[R - 1][t] ^ (uint32_t)j;
+                    continue;
+                }
                 sa[t] = slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane];
                 ca[t] = slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane];
                 sb[t] = slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane];
@@ -289,7 +349,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             }
 #endif
         }
-        if (blk + 1 == nblk) break;
+        if (blk + 1 == nblk || GOL_COOP_DEBUG == 4) continue;
         // ---- hand-off: the band's first and last K rows as granules of parity blk & 1
         const int par = blk & 1;
 #pragma unroll
@@ -429,6 +489,13 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     a.gens = (int)gens;
     a.epoch = epoch & 0xffffu;
     a.err = err;
+    {  // s_sleep periods before the first poll of a hand-off (M <= 2; ld_granules); GOL_COOP_POLL_DELAY for A/B
+        static const int env = [] {
+            const char* e = std::getenv("GOL_COOP_POLL_DELAY");
+            return e ? std::atoi(e) : -1;
+        }();
+        a.poll_delay = env >= 0 ? env : 8;
+    }
     const bool full = a.nl == 64;
     const bool il = ilv == M && M > 1;
     const void* fn = M == 1 ? kernel_m<1>(R, false, bounded, full)
