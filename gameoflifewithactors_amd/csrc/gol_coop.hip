@@ -45,11 +45,6 @@ constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a ba
 #ifndef GOL_COOP_XH
 #define GOL_COOP_XH 1
 #endif
-// Diagnostic builds only (wrong results by design, timing decomposition): 1 no per-generation barrier, 2 no LDS
-// reads, 3 no LDS traffic (barrier kept), 4 no hand-off between bands
-#ifndef GOL_COOP_DEBUG
-#define GOL_COOP_DEBUG 0
-#endif
 constexpr int kSlotRows = GOL_COOP_XH ? 4 : 2;  // LDS words per lane and word of a row, per wave and parity
 // LDS slots per parity: one per wave, plus a zero slot on each side (the neighbours of the first and last
 // waves), so every wave reads its neighbours' slots without a branch
@@ -231,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     const int nblk = (a.gens + K - 1) / K;
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
-        if (blk > 0 && GOL_COOP_DEBUG != 4) {
+        if (blk > 0) {
             // halo rows: the neighbours' edge rows of block blk - 1 (parity (blk - 1) & 1), polled granule by granule
             const int par = (blk - 1) & 1;
             const uint64_t* src[R];
@@ -266,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
 #pragma unroll
             for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
 #pragma unroll
-            for (int t = 0; t < M && GOL_COOP_DEBUG != 3; t++) {
+            for (int t = 0; t < M; t++) {
                 slot[((wv * 4 + 0) * M + t) * 64 + lane] = so[0][t];
                 slot[((wv * 4 + 1) * M + t) * 64 + lane] = co[0][t];
                 slot[((wv * 4 + 2) * M + t) * 64 + lane] = so[R - 1][t];
@@ -285,18 +280,11 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     }
                 }
             }
-            if (GOL_COOP_DEBUG != 1) __syncthreads();
+            __syncthreads();
             if (!active) continue;
             uint32_t sa[M], ca[M], sb[M], cb[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
-                if (GOL_COOP_DEBUG == 2 || GOL_COOP_DEBUG == 3) {
-                    sa[t] = so[0][t] ^ (uint32_t)j;
-                    ca[t] = co[0][t];
-                    sb[t] = so[R - 1][t];
-                    cb[t] = co[R - 1][t] ^ (uint32_t)j;
-                    continue;
-                }
                 sa[t] = slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane];
                 ca[t] = slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane];
                 sb[t] = slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane];
@@ -349,7 +337,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             }
 #endif
         }
-        if (blk + 1 == nblk || GOL_COOP_DEBUG == 4) continue;
+        if (blk + 1 == nblk) continue;  // the last block hands nothing off (continue: the measured instruction stream)
         // ---- hand-off: the band's first and last K rows as granules of parity blk & 1
         const int par = blk & 1;
 #pragma unroll
