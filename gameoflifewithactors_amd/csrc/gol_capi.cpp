@@ -162,9 +162,13 @@ constexpr int64_t kSmallBoardCells = (int64_t)1 << 25;
 constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 // LDS-resident pass (gol_resident.hip) cut-overs, measured on MI355X (profiles/r1/resident_small.log):
 // packed 256^2 0.91 vs 1.47 us/generation on the streaming pass, 512x256 1.23 vs 1.47, but 512^2 1.87 vs
-// 1.49; byte boards 100^2 2.10 vs 3.56, but 255x257 10.7 vs 3.4.
+// 1.49.  Byte boards: off by default.  The ragged boards it could still take (the single-wave pass takes
+// W <= 128 and H <= 256, the reference's 100^2 board included) ran slower on it than on the per-generation
+// byte step in an interleaved A/B: 129x127 3.46 vs 3.10 us/generation, 200x100 3.65 vs 3.10, 181^2 6.26 vs
+// 3.15, 255x257 10.7 vs 3.1; only 255x64 was level, 3.00 vs 3.12 (profiles/r2/byte_cut_ab.log).
+// GOL_RESIDENT_MAX_CELLS still forces it (tests).
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
-constexpr int64_t kResidentBytesMaxCells = (int64_t)1 << 14;
+constexpr int64_t kResidentBytesMaxCells = 0;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
 // Cooperative register-band pass (gol_coop.hip) for packed boards the single-wave pass does not take, up to this
 // many cells and 8192 wide: 4096^2 0.81 vs 1.62 us/generation on the streaming pass, 2048^2 0.44 vs 1.48, 512^2

@@ -97,9 +97,10 @@ int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y);
 int gol_clear(gol_board* b);
 
 /* Advance `generations` synchronous B3/S23 generations (GameOfLifeLogic.fs:47-66 under the Reset->State
- * phase barrier).  Asynchronous with respect to the host; any readback synchronises.  Small boards
- * (packed <= 2^17 cells, bytes <= 2^14; env GOL_RESIDENT_MAX_CELLS overrides) run the whole call as one
- * LDS-resident launch; results are identical either way. */
+ * phase barrier).  Asynchronous with respect to the host; any readback synchronises.  Small and mid-size
+ * boards run the whole call as one launch (single-wave, cooperative or LDS-resident pass: DESIGN.md 4.3;
+ * env GOL_WAVE_RESIDENT, GOL_COOP and GOL_RESIDENT_MAX_CELLS override the cut-overs); results are identical
+ * either way. */
 int gol_step(gol_board* b, int64_t generations);
 int gol_generation(gol_board* b, int64_t* out);
 int gol_synchronize(gol_board* b);
