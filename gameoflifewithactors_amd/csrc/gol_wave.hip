@@ -67,21 +67,41 @@ __global__ __launch_bounds__(64) void gol_wave_resident(const void* __restrict__
 #pragma unroll
         for (int j = 0; j < NW; j++) w[i][j] = 0;
     if (BYTES) {
+        // kBatch owner lanes' rows per round: all their loads are issued before the first ballot, so a round
+        // waits for memory once (one load, one wait, one ballot per 64 cells cost a memory round trip each:
+        // ~30 us of a 100-generation call on the reference's 100^2 board)
+        constexpr int kBatch = 8;
+        constexpr int kChunks = (NW + 1) / 2;
         const uint8_t* cells = static_cast<const uint8_t*>(src);
-        for (int L = 0; L < nl; L++) {
+        for (int L0 = 0; L0 < nl; L0 += kBatch) {
+            uint8_t v[kBatch][RPL][kChunks];
 #pragma unroll
-            for (int i = 0; i < RPL; i++) {
-                const uint8_t* row = cells + (int64_t)(L * RPL + i) * W;
+            for (int b = 0; b < kBatch; b++)
 #pragma unroll
-                for (int c = 0; c < (NW + 1) / 2; c++) {
-                    const int x = 64 * c + lane;
-                    const uint64_t m = __ballot(x < W && row[x] != 0);
-                    if (lane == L) {
-                        w[i][2 * c] = (uint32_t)m;
-                        if (2 * c + 1 < NW) w[i][2 * c + 1] = (uint32_t)(m >> 32);
+                for (int i = 0; i < RPL; i++)
+#pragma unroll
+                    for (int c = 0; c < kChunks; c++) {
+                        // unconditional loads (address clamped into the board, value masked): a branch per load
+                        // would make the compiler wait for each
+                        // (owner lanes past the last active lane load a clamped row and keep garbage: no active
+                        // lane reads them, and they are never stored)
+                        const int x = 64 * c + lane;
+                        const int L = L0 + b < nl ? L0 + b : nl - 1;
+                        const uint8_t t = cells[(int64_t)(L * RPL + i) * W + (x < W ? x : W - 1)];
+                        v[b][i][c] = x < W ? t : (uint8_t)0;
                     }
-                }
-            }
+#pragma unroll
+            for (int b = 0; b < kBatch; b++)
+#pragma unroll
+                for (int i = 0; i < RPL; i++)
+#pragma unroll
+                    for (int c = 0; c < kChunks; c++) {
+                        const uint64_t m = __ballot(v[b][i][c] != 0);
+                        if (lane == L0 + b) {
+                            w[i][2 * c] = (uint32_t)m;
+                            if (2 * c + 1 < NW) w[i][2 * c + 1] = (uint32_t)(m >> 32);
+                        }
+                    }
         }
     } else if (active) {
 #pragma unroll
