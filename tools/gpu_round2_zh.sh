@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 2, call zh: single-wave pass with the byte board's loads batched (8 owner lanes' rows in flight per
+# Round 2, call zh (and zi: 16 owner lanes per round against 8): single-wave pass with the byte loads batched (owner lanes rows in flight per
 # round): wave-pass and parity tests, config-1 call latency against the previous build.
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 bash tools/gpu_steps.sh \
