@@ -236,6 +236,8 @@ struct gol_board {
     uint32_t* coop_xch = nullptr;       // cooperative pass: hand-off granules (allocated on first use)
     int64_t coop_xch_words = 0;
     unsigned coop_epoch = 0;            // tag epoch of the last cooperative launch (1..65535)
+    uint32_t* rag[2] = {nullptr, nullptr};  // ragged byte boards on the cooperative pass: whole-word scratch rows
+    int64_t rag_words = 0;                  // capacity of each rag buffer
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -376,6 +378,71 @@ bool use_coop(const gol_board* b) {
            gol::coop_plan(b->W, b->H, coop_depth(b), &nwg, &B, &R) && nwg < kCoopFlagWords;
 }
 
+// Words per lane of the cooperative pass for a ragged row of nw words (rows padded to a multiple of it).
+int coop_m_ragged(int64_t nw) { return nw <= 64 ? 1 : (nw <= 128 ? 2 : (nw <= 256 ? 4 : 0)); }
+
+// Ragged byte boards (width not a multiple of 32) the single-wave pass does not take run on the cooperative pass
+// through whole-word scratch rows when a call has at least this many generations: the per-generation byte step
+// costs ~3.1 us per generation (profiles/r2/byte_cut_ab.log), the pack / unpack launches around the pass a few
+// generations' worth.
+constexpr int64_t kCoopRaggedMinGens = 16;
+bool use_coop_ragged(const gol_board* b, int64_t* pitch) {
+    if (!coop_enabled() || b->packed || b->W % 32 == 0) return false;
+    const char* m = std::getenv("GOL_COOP_MAX_CELLS");
+    const int64_t maxc = m ? (int64_t)std::atoll(m) : kCoopMaxCells;
+    const int64_t nw = (b->W + 31) / 32;
+    const int cm = coop_m_ragged(nw);
+    if (!cm || b->W * b->H > maxc) return false;
+    const int64_t nwp = (nw + cm - 1) / cm * cm;
+    int nwg = 0, B = 0, R = 0;
+    if (!gol::coop_plan(nwp * 32, b->H, coop_depth(b), &nwg, &B, &R) || nwg >= kCoopFlagWords) return false;
+    *pitch = nwp;
+    return true;
+}
+
+// `gens` generations of the cooperative pass on packed rows of W cells (`pitch` words, layout `ilv`; ragged_w > 0:
+// scratch rows of a ragged board of that width), ping-ponging between bufs[*cur] and bufs[*cur ^ 1]; *cur ends on
+// the result.  One launch per kCoopMaxGensPerLaunch generations.
+int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w, uint32_t* const bufs[2], int* cur,
+               int64_t gens) {
+    if (!b->coop) {
+        GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
+        GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
+    }
+    int nwg = 0, B = 0, R = 0;
+    const int k = coop_depth(b);
+    (void)gol::coop_plan(W, b->H, k, &nwg, &B, &R);
+    const int64_t need = gol::coop_xch_words(W, nwg, k);
+    if (need > b->coop_xch_words) {
+        if (b->coop_xch) {
+            GOL_HIP(hipStreamSynchronize(b->stream));
+            GOL_HIP(hipFree(b->coop_xch));
+            b->coop_xch = nullptr;
+            b->coop_xch_words = 0;
+        }
+        GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
+        b->coop_xch_words = need;
+        b->coop_epoch = 0xffff;  // forces the clear below: a fresh buffer holds arbitrary tags
+    } else if (const char* e0 = std::getenv("GOL_COOP_EPOCH")) {
+        // tests: the next launch's epoch (runs the 16-bit wrap, and the clear of the granules it needs, early)
+        b->coop_epoch = (unsigned)std::atoi(e0) & 0xffffu;
+    }
+    while (gens > 0) {
+        const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;
+        if (++b->coop_epoch > 0xffff) {  // tags of an earlier epoch could match again: clear the granules
+            GOL_HIP(hipMemsetAsync(b->coop_xch, 0, (size_t)b->coop_xch_words * sizeof(uint32_t), b->stream));
+            b->coop_epoch = 1;
+        }
+        GOL_HIP(gol::launch_coop_pass(bufs[*cur], bufs[*cur ^ 1], W, b->H, pitch, ilv, k, g, b->boundary == GOL_BOUNDED,
+                                      b->coop_epoch, reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
+                                      b->coop_xch_words, b->stream, ragged_w));
+        *cur ^= 1;
+        b->generation += g;
+        gens -= g;
+    }
+    return GOL_OK;
+}
+
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
     if (gens > 0 && use_wave_resident(b)) {
@@ -390,42 +457,28 @@ int step_impl(gol_board* b, int64_t gens) {
         return GOL_OK;
     }
     if (gens > 0 && use_coop(b)) {
-        if (!b->coop) {
-            GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
-            GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
-        }
-        int nwg = 0, B = 0, R = 0;
-        const int k = coop_depth(b);
-        (void)gol::coop_plan(b->W, b->H, k, &nwg, &B, &R);
-        const int64_t need = gol::coop_xch_words(b->W, nwg, k);
-        if (need > b->coop_xch_words) {
-            if (b->coop_xch) {
-                GOL_HIP(hipStreamSynchronize(b->stream));
-                GOL_HIP(hipFree(b->coop_xch));
-                b->coop_xch = nullptr;
-                b->coop_xch_words = 0;
+        uint32_t* bufs[2] = {b->words(0), b->words(1)};
+        return coop_steps(b, b->W, b->pitch, b->ilv, 0, bufs, &b->cur, gens);
+    }
+    int64_t rag_pitch = 0;
+    if (gens >= kCoopRaggedMinGens && use_coop_ragged(b, &rag_pitch)) {
+        // the ragged byte board as whole words in scratch rows, the pass, and back to bytes
+        const int64_t need = rag_pitch * b->H;
+        if (need > b->rag_words) {
+            GOL_HIP(hipStreamSynchronize(b->stream));
+            for (uint32_t*& r : b->rag) {
+                if (r) GOL_HIP(hipFree(r));
+                r = nullptr;
             }
-            GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
-            b->coop_xch_words = need;
-            b->coop_epoch = 0xffff;  // forces the clear below: a fresh buffer holds arbitrary tags
-        } else if (const char* e0 = std::getenv("GOL_COOP_EPOCH")) {
-            // tests: the next launch's epoch (runs the 16-bit wrap, and the clear of the granules it needs, early)
-            b->coop_epoch = (unsigned)std::atoi(e0) & 0xffffu;
+            b->rag_words = 0;
+            for (uint32_t*& r : b->rag) GOL_HIP(hipMalloc(&r, (size_t)need * sizeof(uint32_t)));
+            b->rag_words = need;
         }
-        while (gens > 0) {
-            const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;
-            if (++b->coop_epoch > 0xffff) {  // tags of an earlier epoch could match again: clear the granules
-                GOL_HIP(hipMemsetAsync(b->coop_xch, 0, (size_t)b->coop_xch_words * sizeof(uint32_t), b->stream));
-                b->coop_epoch = 1;
-            }
-            GOL_HIP(gol::launch_coop_pass(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, b->ilv, k, g,
-                                          b->boundary == GOL_BOUNDED, b->coop_epoch,
-                                          reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
-                                          b->coop_xch_words, b->stream));
-            b->cur ^= 1;
-            b->generation += g;
-            gens -= g;
-        }
+        GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, rag_pitch, b->stream));
+        int rc_cur = 0;
+        if (int rc = coop_steps(b, rag_pitch * 32, rag_pitch, 1, b->W, b->rag, &rc_cur, gens)) return rc;
+        GOL_HIP(gol::launch_unpack_ragged(b->rag[rc_cur], b->cells(b->cur ^ 1), b->W, b->H, rag_pitch, b->stream));
+        b->cur ^= 1;
         return GOL_OK;
     }
     if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
@@ -495,6 +548,8 @@ void free_board(gol_board* b) {
     if (b->acc) (void)hipFree(b->acc);
     if (b->coop) (void)hipFree(b->coop);
     if (b->coop_xch) (void)hipFree(b->coop_xch);
+    for (uint32_t* r : b->rag)
+        if (r) (void)hipFree(r);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }

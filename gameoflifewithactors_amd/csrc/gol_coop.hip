@@ -65,6 +65,8 @@ struct CoopArgs {
     unsigned epoch;       // launch epoch (16 bits) of the granule tags
     int poll_delay;       // s_sleep 1 periods (64 clocks) before the first poll of a hand-off
     int* err;             // set to 1 by a timed-out wait
+    int rag_lb;           // ragged rows (kLayRagged): bit of the last cell in the last word, (W - 1) & 31
+    int rag_last;         // ragged rows: index of the last word that holds cells, ceil(W / 32) - 1
 };
 
 // A lane's M words of one row as granules {word, tag}, write-through (8-byte sc1 stores)
@@ -171,8 +173,49 @@ __device__ __forceinline__ void lane_row_sum(const uint32_t (&r)[M], int lane, i
     for (int j = 0; j < M; j++) row_sum(j == 0 ? left : r[j - 1], r[j], j == M - 1 ? right : r[j + 1], s[j], c[j]);
 }
 
-template <int M, int R, bool ILV, bool BOUNDED, bool FULL>
+// Word layouts of a band row: consecutive words of an ilv-1 board, interleaved blocks of an ilv-M board, or the
+// consecutive words of a ragged row (width not a multiple of 32: the byte board packed by the host into a scratch
+// buffer of whole words, cells past W zero, the row end fixed up at bit level).
+constexpr int kLayWords = 0, kLayInterleaved = 1, kLayRagged = 2;
+
+// Horizontal 3-sums of a lane's M consecutive words of a ragged row (GameOfLifeDriver.fs:21-25 on a torus: the
+// west neighbour of cell 0 is cell W - 1, bit `lb` of word `last`, held by lane lane_last at position t_last;
+// the east neighbour of cell W - 1 is cell 0; Script.fsx:6-13 when bounded: dead beyond both ends).  The lanes
+// exchange edge words with zero fill; the two row-end words are then patched, as in the single-wave pass
+// (gol_wave.hip).
+template <int M, bool BOUNDED>
+__device__ __forceinline__ void ragged_row_sum(const uint32_t (&r)[M], int lane, int lane_last, int t_last, int lb,
+                                               uint32_t (&s)[M], uint32_t (&c)[M]) {
+    const uint32_t left = (uint32_t)__builtin_amdgcn_mov_dpp((int)r[M - 1], 0x138, 0xf, 0xf, true);  // wave_shr:1
+    const uint32_t right = (uint32_t)__builtin_amdgcn_mov_dpp((int)r[0], 0x130, 0xf, 0xf, true);     // wave_shl:1
+    uint32_t west[M], east[M];
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        west[t] = align_right(r[t], t == 0 ? left : r[t - 1], 31);
+        east[t] = align_right(t == M - 1 ? right : r[t + 1], r[t], 1);
+    }
+    if (!BOUNDED) {
+        uint32_t lw = r[0];
+#pragma unroll
+        for (int t = 1; t < M; t++) lw = t == t_last ? r[t] : lw;
+        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)lw, lane_last);
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)r[0], 0);
+        if (lane == 0) west[0] = (r[0] << 1) | ((last >> lb) & 1u);
+#pragma unroll
+        for (int t = 0; t < M; t++)
+            if (lane == lane_last && t == t_last) east[t] = (r[t] >> 1) | ((first & 1u) << lb);
+    }
+#pragma unroll
+    for (int t = 0; t < M; t++) {
+        s[t] = lut3<0x96>(west[t], r[t], east[t]);
+        c[t] = lut3<0xE8>(west[t], r[t], east[t]);
+    }
+}
+
+template <int M, int R, int LAY, bool BOUNDED, bool FULL>
 __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
+    constexpr bool ILV = LAY == kLayInterleaved;
+    constexpr bool RAG = LAY == kLayRagged;
     extern __shared__ uint32_t xs[];  // [2 parity][kSlots][kSlotRows][M][64 lanes]; slots 0 and kSlots - 1 stay zero
     const int band = blockIdx.x;
     const int lane = threadIdx.x & 63;
@@ -186,6 +229,18 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     const int nl = a.nl;
     const bool lane_on = FULL || lane < nl;  // full rows: every lane holds words
     const int col = lane * M;  // this lane's first word
+    // ragged rows: the lane holding the last word, its position there, and per word the mask of cells on the row
+    // (the other layouts compile none of this: their instruction streams are the measured ones)
+    [[maybe_unused]] int lane_last = 0, t_last = 0;
+    [[maybe_unused]] uint32_t wmask[M];
+    if constexpr (RAG) {
+        lane_last = a.rag_last / M;
+        t_last = a.rag_last % M;
+        const uint32_t lastmask = a.rag_lb == 31 ? 0xffffffffu : (2u << a.rag_lb) - 1u;
+#pragma unroll
+        for (int t = 0; t < M; t++)
+            wmask[t] = col + t < a.rag_last ? 0xffffffffu : (col + t == a.rag_last ? lastmask : 0u);
+    }
     const int up = band > 0 ? band - 1 : (BOUNDED ? -1 : a.nwg - 1);
     const int dn = band + 1 < a.nwg ? band + 1 : (BOUNDED ? -1 : 0);
     auto gy_of = [&](int i) { return y0 - K + i; };
@@ -259,7 +314,12 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             // every wave publishes the row sums of its first and last rows (inactive waves too: their rows border
             // active ones), so no wave re-sums a neighbour's row
 #pragma unroll
-            for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+            for (int i = 0; i < R; i++) {
+                if constexpr (RAG)
+                    ragged_row_sum<M, BOUNDED>(w[i], lane, lane_last, t_last, a.rag_lb, so[i], co[i]);
+                else
+                    lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+            }
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 slot[((wv * 4 + 0) * M + t) * 64 + lane] = so[0][t];
@@ -276,7 +336,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     for (int t = 0; t < M; t++) {
                         const uint32_t v = life_next(so[i - 1][t], co[i - 1][t], so[i][t], co[i][t], so[i + 1][t],
                                                      co[i + 1][t], w[i][t]);
-                        w[i][t] = dead || !lane_on ? 0u : v;
+                        w[i][t] = dead || !lane_on ? 0u : (RAG ? v & wmask[t] : v);
                     }
                 }
             }
@@ -300,7 +360,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     const uint32_t v = life_next(i == 0 ? sa[t] : so[i - 1][t], i == 0 ? ca[t] : co[i - 1][t], so[i][t],
                                                  co[i][t], i == R - 1 ? sb[t] : so[i + 1][t],
                                                  i == R - 1 ? cb[t] : co[i + 1][t], w[i][t]);
-                    w[i][t] = dead || !lane_on ? 0u : v;
+                    w[i][t] = dead || !lane_on ? 0u : (RAG ? v & wmask[t] : v);
                 }
             }
 #else
@@ -311,7 +371,12 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             }
             if (active) {
 #pragma unroll
-                for (int i = 0; i < R; i++) lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+                for (int i = 0; i < R; i++) {
+                if constexpr (RAG)
+                    ragged_row_sum<M, BOUNDED>(w[i], lane, lane_last, t_last, a.rag_lb, so[i], co[i]);
+                else
+                    lane_row_sum<M, ILV, BOUNDED, FULL>(w[i], lane, nl, so[i], co[i]);
+            }
             }
             __syncthreads();  // a barrier per generation: LDS counters per neighbour wave measured 0.90 vs 0.56 us
             if (!active) continue;
@@ -322,7 +387,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                 below[t] = slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane];
             }
             uint32_t sa[M], ca[M], sb[M], cb[M];
-            lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sa, ca);
+            lane_row_sum<M, ILV, BOUNDED, FULL>(above, lane, nl, sa, ca);  // (raw-row A/B variant: no ragged rows)
             lane_row_sum<M, ILV, BOUNDED, FULL>(below, lane, nl, sb, cb);
 #pragma unroll
             for (int i = 0; i < R; i++) {
@@ -332,7 +397,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     const uint32_t v = life_next(i == 0 ? sa[t] : so[i - 1][t], i == 0 ? ca[t] : co[i - 1][t], so[i][t],
                                                  co[i][t], i == R - 1 ? sb[t] : so[i + 1][t],
                                                  i == R - 1 ? cb[t] : co[i + 1][t], w[i][t]);
-                    w[i][t] = dead || !lane_on ? 0u : v;
+                    w[i][t] = dead || !lane_on ? 0u : (RAG ? v & wmask[t] : v);
                 }
             }
 #endif
@@ -377,35 +442,36 @@ int coop_cus() {
 
 constexpr int kRows[] = {1, 2, 3, 4, 6, 8};  // rows per wave instantiated
 
-template <int M, int R, bool ILV>
+template <int M, int R, int LAY>
 const void* kernel_mri(bool bounded, bool full) {
+    if (LAY == kLayRagged)  // ragged rows never use the full-wave rotate (the row end is patched at bit level)
+        return bounded ? (const void*)&gol_band_pass<M, R, LAY, true, false> : (const void*)&gol_band_pass<M, R, LAY, false, false>;
     if (bounded)
-        return full ? (const void*)&gol_band_pass<M, R, ILV, true, true> : (const void*)&gol_band_pass<M, R, ILV, true, false>;
-    return full ? (const void*)&gol_band_pass<M, R, ILV, false, true> : (const void*)&gol_band_pass<M, R, ILV, false, false>;
+        return full ? (const void*)&gol_band_pass<M, R, LAY, true, true> : (const void*)&gol_band_pass<M, R, LAY, true, false>;
+    return full ? (const void*)&gol_band_pass<M, R, LAY, false, true> : (const void*)&gol_band_pass<M, R, LAY, false, false>;
+}
+
+template <int M, int LAY>
+const void* kernel_ml(int r, bool bounded, bool full) {
+    switch (r) {
+        case 1: return kernel_mri<M, 1, LAY>(bounded, full);
+        case 2: return kernel_mri<M, 2, LAY>(bounded, full);
+        case 3: return kernel_mri<M, 3, LAY>(bounded, full);
+        case 4: return kernel_mri<M, 4, LAY>(bounded, full);
+        case 6: return kernel_mri<M, 6, LAY>(bounded, full);
+        case 8: return kernel_mri<M, 8, LAY>(bounded, full);
+    }
+    return nullptr;
 }
 
 template <int M>
-const void* kernel_m(int r, bool ilv, bool bounded, bool full) {
-    if (M > 1 && ilv) {  // interleaved boards (ilv == M)
-        switch (r) {
-            case 1: return kernel_mri<M, 1, true>(bounded, full);
-            case 2: return kernel_mri<M, 2, true>(bounded, full);
-            case 3: return kernel_mri<M, 3, true>(bounded, full);
-            case 4: return kernel_mri<M, 4, true>(bounded, full);
-            case 6: return kernel_mri<M, 6, true>(bounded, full);
-            case 8: return kernel_mri<M, 8, true>(bounded, full);
-        }
+const void* kernel_m(int r, int lay, bool bounded, bool full) {
+    if (lay == kLayInterleaved) {  // interleaved boards (ilv == M)
+        if constexpr (M > 1) return kernel_ml<M, kLayInterleaved>(r, bounded, full);
         return nullptr;
     }
-    switch (r) {
-        case 1: return kernel_mri<M, 1, false>(bounded, full);
-        case 2: return kernel_mri<M, 2, false>(bounded, full);
-        case 3: return kernel_mri<M, 3, false>(bounded, full);
-        case 4: return kernel_mri<M, 4, false>(bounded, full);
-        case 6: return kernel_mri<M, 6, false>(bounded, full);
-        case 8: return kernel_mri<M, 8, false>(bounded, full);
-    }
-    return nullptr;
+    if (lay == kLayRagged) return kernel_ml<M, kLayRagged>(r, bounded, full);
+    return kernel_ml<M, kLayWords>(r, bounded, full);
 }
 
 }  // namespace
@@ -456,7 +522,7 @@ int64_t coop_xch_words(int64_t W, int nwg, int k) { return (int64_t)2 * 2 * nwg 
 
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
-                            hipStream_t s) {
+                            hipStream_t s, int64_t ragged_w) {
     int nwg = 0, B = 0, R = 0;
     if (!coop_plan(W, H, k, &nwg, &B, &R) || gens < 1 || gens > 65535 || pitch < W / 32 ||
         coop_xch_words(W, nwg, k) > xch_words)
@@ -464,6 +530,8 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     const int nw = (int)(W / 32);
     const int M = coop_m(nw);
     if (ilv != 1 && ilv != M) return hipErrorInvalidValue;
+    // ragged rows: W is the padded width of the scratch rows (whole words, a multiple of M), ragged_w the board's
+    if (ragged_w && (ilv != 1 || ragged_w > W || ragged_w <= W - 32 * M)) return hipErrorInvalidValue;
     CoopArgs a;
     a.src = src;
     a.dst = dst;
@@ -477,6 +545,8 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     a.gens = (int)gens;
     a.epoch = epoch & 0xffffu;
     a.err = err;
+    a.rag_lb = ragged_w ? (int)((ragged_w - 1) & 31) : 31;
+    a.rag_last = ragged_w ? (int)((ragged_w + 31) / 32 - 1) : nw - 1;
     {  // s_sleep periods before the first poll of a hand-off (M <= 2; ld_granules); GOL_COOP_POLL_DELAY for A/B
         static const int env = [] {
             const char* e = std::getenv("GOL_COOP_POLL_DELAY");
@@ -485,9 +555,9 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
         a.poll_delay = env >= 0 ? env : 8;
     }
     const bool full = a.nl == 64;
-    const bool il = ilv == M && M > 1;
-    const void* fn = M == 1 ? kernel_m<1>(R, false, bounded, full)
-                            : (M == 2 ? kernel_m<2>(R, il, bounded, full) : kernel_m<4>(R, il, bounded, full));
+    const int lay = ragged_w ? kLayRagged : (ilv == M && M > 1 ? kLayInterleaved : kLayWords);
+    const void* fn = M == 1 ? kernel_m<1>(R, lay, bounded, full)
+                            : (M == 2 ? kernel_m<2>(R, lay, bounded, full) : kernel_m<4>(R, lay, bounded, full));
     if (!fn) return hipErrorInvalidValue;
     const size_t need = (size_t)2 * kSlots * kSlotRows * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;

@@ -56,6 +56,36 @@ __global__ void gol_pack(const uint8_t* __restrict__ cells, uint32_t* __restrict
     words[(row0 + y) * pitch + w] = v;
 }
 
+// Ragged byte board (any width) -> whole consecutive words (the cooperative pass's scratch rows): one thread
+// per word of the `pitch`-word row, cells past W and words past ceil(W / 32) zero
+__global__ void gol_pack_ragged(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words, int64_t W, int64_t H,
+                                int64_t pitch) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= pitch * H) return;
+    const int64_t w = idx % pitch, y = idx / pitch;
+    const uint8_t* p = cells + y * W;
+    uint32_t v = 0;
+    for (int b = 0; b < 32; b++) {
+        const int64_t x = 32 * w + b;
+        if (x < W) v |= (uint32_t)(p[x] != 0) << b;
+    }
+    words[idx] = v;
+}
+// ... and back: the W cells of each row as 0 / 1 bytes (the byte board's own values)
+__global__ void gol_unpack_ragged(const uint32_t* __restrict__ words, uint8_t* __restrict__ cells, int64_t W, int64_t H,
+                                  int64_t pitch) {
+    const int64_t nw = (W + 31) / 32;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nw * H) return;
+    const int64_t w = idx % nw, y = idx / nw;
+    const uint32_t v = words[y * pitch + w];
+    uint8_t* p = cells + y * W;
+    for (int b = 0; b < 32; b++) {
+        const int64_t x = 32 * w + b;
+        if (x < W) p[x] = (uint8_t)((v >> b) & 1u);
+    }
+}
+
 // packed -> bytes: out[x + y*stride] = alive ? value : 0; one thread per stored word
 __global__ void gol_unpack(const uint32_t* __restrict__ words, uint8_t* __restrict__ out, int64_t W, int64_t rows,
                            int64_t pitch, int64_t row0, int64_t stride, uint8_t value, int ilv) {
@@ -288,6 +318,17 @@ hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_
 hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                        int ilv, hipStream_t s) {
     hipLaunchKernelGGL(gol_pack, dim3(grid1d(W / 32 * rows)), dim3(256), 0, s, cells, words, W, rows, pitch, row0, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_ragged(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int64_t pitch, hipStream_t s) {
+    hipLaunchKernelGGL(gol_pack_ragged, dim3(grid1d(pitch * H)), dim3(256), 0, s, cells, words, W, H, pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int64_t pitch,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(gol_unpack_ragged, dim3(grid1d((W + 31) / 32 * H)), dim3(256), 0, s, words, cells, W, H, pitch);
     return hipGetLastError();
 }
 

@@ -40,6 +40,11 @@ hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, 
 hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s);
 hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                        int ilv, hipStream_t s);
+// byte board (any width W) <-> consecutive words, `pitch` words per row: bit b of word j = cell 32 j + b, cells past
+// W (and whole words past ceil(W / 32)) zero; unpack writes 0 / 1 for the W cells of each row
+hipError_t launch_pack_ragged(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int64_t pitch, hipStream_t s);
+hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int64_t pitch,
+                                hipStream_t s);
 hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                          int64_t stride, uint8_t value, int ilv, hipStream_t s);
 hipError_t launch_region(const void* board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
@@ -77,10 +82,12 @@ int coop_k();
 int coop_m(int64_t nw);  // words per lane for rows of nw words (0: too wide for the pass)
 bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R);
 int64_t coop_xch_words(int64_t W, int nwg, int k);  // exchange buffer the pass needs
-// gens <= 65535 per launch; epoch (1..65535) tags this launch's hand-off granules (clear xch before reusing one)
+// gens <= 65535 per launch; epoch (1..65535) tags this launch's hand-off granules (clear xch before reusing one).
+// ragged_w > 0: a ragged board (width ragged_w, not a multiple of 32) packed into whole-word scratch rows of W cells
+// (launch_pack_ragged), ilv 1; 0: a packed board of width W.
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
-                            hipStream_t s);
+                            hipStream_t s, int64_t ragged_w = 0);
 
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
 int wave_resident_rpl(int64_t W, int64_t H);  // rows per lane, 0 = the board does not fit

@@ -7,7 +7,8 @@ Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus GameOfLifeDri
 Script.fsx:6-13), the BASELINE config-2 golden checkpoints (4096^2, .NET Random seed 42, 10k generations), and
 the streaming pass on the same board (GOL_COOP=0).  Uneven bands (heights that do not divide over the CUs),
 bands shorter than two blocks, several block depths (GOL_COOP_K), both word layouts (consecutive words of an
-ilv-1 board, interleaved blocks of an ilv-2 / ilv-4 board) and split calls are covered.
+ilv-1 board, interleaved blocks of an ilv-2 / ilv-4 board), ragged byte boards (widths not a multiple of 32,
+through whole-word scratch rows) and split calls are covered.
 """
 import json
 import os
@@ -122,3 +123,35 @@ def test_coop_epoch_wrap(gol, oracle):
         done += 17
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, done, 0))
 
+
+
+@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("w,h", [(129, 300), (1001, 257), (2047, 90), (2049, 131), (4095, 64), (4097, 77),
+                                 (8191, 40), (333, 1000)])
+def test_coop_ragged_widths(gol, oracle, w, h, boundary):
+    """Byte boards of widths that are not a multiple of 32 and that the single-wave pass does not take run on
+    the cooperative pass through whole-word scratch rows (calls of >= 16 generations), with the row end patched
+    at bit level: torus wrap from cell W - 1 to cell 0 (GameOfLifeDriver.fs:21-25), dead beyond both ends when
+    bounded (Script.fsx:6-13).  Rows of 1, 2 and 4 words per lane, padded rows (2049, 4097), split calls and a
+    remainder block, against the oracle and against the per-generation byte step (GOL_COOP=0)."""
+    b0 = _rand(h, w, w + 7 * h + boundary)
+    steps = [16, 3, 21]  # 3 < 16: the byte step between two pass calls
+    want = oracle.c_run(b0, sum(steps), boundary)
+    for coop in (True, False):
+        with _Env(GOL_COOP="1" if coop else "0"), gol.Board(w, h, boundary) as b:
+            assert not b.info()["packed"]
+            b.set_cells(b0)
+            for g in steps:
+                b.step(g)
+            assert b.generation == sum(steps)
+            np.testing.assert_array_equal(b.get_cells(), want, err_msg=f"coop={coop}")
+
+
+def test_coop_ragged_byte_values(gol, oracle):
+    """Byte cells are alive when nonzero (any value); the ragged pass writes the board back as 0 / 1."""
+    b0 = _rand(200, 1001, 5)
+    vals = (b0 * np.random.default_rng(6).integers(1, 256, size=b0.shape)).astype(np.uint8)
+    with _Env(GOL_COOP="1"), gol.Board(1001, 200, 0) as b:
+        b.set_cells(vals)
+        b.step(24)
+        np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 24, 0))
