@@ -10,6 +10,10 @@ process per GPU under torchrun) the board is 65536 wide and 65536*N tall, split 
     python bench.py                          # N = 1: 10k generations timed (~0.5 s), under a minute in all
     python bench.py --steps 64 --warmup 4 --tblock 16
     torchrun --nproc-per-node 8 bench.py --gpus 8
+    # BASELINE configs 2 and 5 on the C-ABI board (the product's pass choice), one gol_step call per step:
+    python bench.py --init dotnet-mod2 --seed 42 --width 4096 --height 4096 --generations 1000 --steps 5
+    python bench.py --init rle:gosper-gun@1000,1000+r-pentomino@3000,3000 --width 4096 --height 4096 \
+        --generations 100000 --steps 1 --warmup 1
 
 Prints ONE JSON line (rank 0).  Inputs are resident in HBM before the timed region; the timed region is
 bracketed by barrier + device synchronize on both sides, max over ranks.
@@ -17,6 +21,7 @@ bracketed by barrier + device synchronize on both sides, max over ranks.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import platform
@@ -75,6 +80,12 @@ def parse():
                    help="skip the on-box race between the AUTOTUNE depths (default: race them during warmup, "
                    "interleaved, and time the faster; agreed across ranks) and use the engine default depth")
     p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--init", default="splitmix",
+                   help="board init: splitmix (device-side, the default), dotnet-mod2 (GameOfLifeDriver.fs:9-19), "
+                   "dotnet-next2 (Script.fsx:25-27), or rle:SPEC[+SPEC] with SPEC = FILE|gosper-gun|r-pentomino[@x,y]; "
+                   "anything but splitmix times the C-ABI board (gol_step: the pass the product picks for the size)")
+    p.add_argument("--gens-per-step", type=int, default=0,
+                   help="board leg (--init other than splitmix): generations per gol_step call (0 = --generations)")
     p.add_argument("--boundary", choices=["torus", "bounded"], default="torus")
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="CPU baseline sample length (C2 actor sample, fair-CPU sample)")
@@ -85,6 +96,9 @@ def parse():
                    help="N > 1: nccl (= RCCL over xGMI, the product path) or gloo (host-staged halo; lets "
                    "several ranks share one GPU in rehearsals)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--handle-leg-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--handle-timeout", type=float, default=300.0,
+                   help="seconds the one-process handle leg (a child process of rank 0) may take")
     p.add_argument("--handle-parts", type=int, default=-1,
                    help="one-process C-ABI leg (gol_create_multi, csrc/gol_multi.cpp: what the F# drop-in calls): "
                    "the same board in P row strips on devices 0..P-1 (round-robin over the visible devices, so "
@@ -124,7 +138,9 @@ def cpu_baseline(args):
     exe, fast = os.path.join(odir, "actor_protocol"), os.path.join(odir, "gol_fast_bench")
     if not (os.path.exists(exe) and os.path.exists(fast)):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # the box's CPU share is 16 threads per GPU (OMP_NUM_THREADS there); the host itself has more cores
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(16, avail))
     cpu = _cpu_model()
     c1 = {}
     for seed in (0, 1, 42):
@@ -134,6 +150,11 @@ def cpu_baseline(args):
     n2 = str(args.cpu_c2)
     c2 = _run_json([exe, n2, n2, "0", str(threads), "42", str(args.cpu_seconds), "dotnet-mod2"])
     fair = _run_json([fast, str(args.width), str(args.width), "0", str(threads), str(args.cpu_seconds)])
+    # the same stepper on every CPU this process may run on (the whole host unless the box restricts it)
+    fair_all = None
+    if avail > threads:
+        fair_all = _run_json([fast, str(args.width), str(args.width), "0", str(avail), str(args.cpu_seconds)])
+    host = {"logical_cpus": os.cpu_count(), "cpus_available": avail, "model": cpu}
     return {
         "value": c2["cell_updates_per_s"] / 1e9,
         "unit": "GCUPS",
@@ -156,6 +177,14 @@ def cpu_baseline(args):
             "sample": f"bit-sliced carry-save stepper (oracle/gol_fast.c, AVX-512 build), {fair['width']}x"
             f"{fair['height']} torus splitmix 0x5EED, {fair['generations']} generations in {fair['seconds']:.1f} s",
         },
+        "fair_cpu_all_cpus": None if fair_all is None else {
+            "value": fair_all["cell_updates_per_s"] / 1e9,
+            "unit": "GCUPS",
+            "cores": avail,
+            "sample": f"the same stepper on all {avail} available CPUs, {fair_all['generations']} generations in "
+            f"{fair_all['seconds']:.1f} s",
+        },
+        "host": host,
     }
 
 
@@ -168,6 +197,7 @@ def handle_leg(args, W, H, boundary, parts, ndev):
     devices = [i % ndev for i in range(parts)]
     with Board(W, H, boundary, devices=devices) as b:
         k = b.parts()[0]["ghost"] if parts > 1 else b.info()["tblock_k"]
+        transport = b.transport()
         b.seed_splitmix(args.seed)
         b.step(args.warmup * k)
         b.synchronize()
@@ -183,23 +213,139 @@ def handle_leg(args, W, H, boundary, parts, ndev):
         "generations_per_step": k,
         "strips": parts,
         "devices": devices,
-        "transport": "hipMemcpyPeerAsync halo rows (xGMI peer copies), one process",
+        "transport": transport,
         "pass_timing_us": timing,
         "edge_wait_us_max": max(t["edge_wait_us"] for t in timing),
     }
 
 
-def load_traffic(path, key):
+def run_handle_leg(args, W, H, boundary, parts, ndev):
+    """The handle leg in a child process of rank 0 under a time limit: with N > 1 distinct GPUs it creates an RCCL
+    communicator over all of them inside one process, and a failure or hang there must not cost the main line."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--handle-leg-child", "--width", str(W), "--height", str(H),
+           "--boundary", args.boundary, "--handle-parts", str(parts), "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--seed", str(args.seed)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
+    env["WORLD_SIZE"] = "1"
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.handle_timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"handle leg exceeded {args.handle_timeout:.0f} s (killed)"}
+    if r.returncode != 0:
+        return {"error": f"handle leg exited {r.returncode}: {r.stderr.strip()[-600:]}"}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def traffic_key(W, rows, boundary, k, ilv):
+    return f"{W}x{rows}_{boundary}_k{k}_m{ilv}"
+
+
+def load_traffic(path, key, fingerprint):
+    """The PMC measurement for this configuration, only if it was taken on this build's device code."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(key)
     except (OSError, ValueError):
         return None
+    e = d.get(key)
+    if not e or not fingerprint or e.get("device_code") != fingerprint:
+        return None
+    return e
+
+
+def board_leg(args) -> dict:
+    """BASELINE configs 1, 2 and 5 on the C-ABI board (what the F# drop-in calls): the board the reference seeds
+    (--init), one gol_step call of --gens-per-step generations per step, so the engine picks the pass it picks for
+    the size (single-wave, cooperative, LDS-resident or streaming).  Host wall time around the timed calls and HIP
+    events on the board's stream.  N = 1 only."""
+    import torch
+
+    from gameoflifewithactors_amd import BOUNDED, INIT_DOTNET_MOD2, INIT_DOTNET_NEXT2, TORUS, Board, patterns
+
+    W, H = args.width, args.height
+    boundary = TORUS if args.boundary == "torus" else BOUNDED
+    gps = args.gens_per_step or args.generations
+    steps = args.steps if args.steps > 0 else 1
+    with Board(W, H, boundary) as b:
+        if args.init == "dotnet-mod2":
+            b.seed_dotnet(args.seed, INIT_DOTNET_MOD2)
+        elif args.init == "dotnet-next2":
+            b.seed_dotnet(args.seed, INIT_DOTNET_NEXT2)
+        elif args.init.startswith("rle:"):
+            for text, x, y in patterns.parse_placements(args.init[4:]):
+                b.place_rle(text, x, y)
+        else:
+            raise SystemExit(f"unknown --init {args.init}")
+        h0 = b.hash()
+        for _ in range(args.warmup):
+            b.step(gps)
+        b.synchronize()
+        first = b.generation
+        s = torch.cuda.ExternalStream(b.stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(s)
+        for _ in range(steps):
+            b.step(gps)
+        e1.record(s)
+        b.synchronize()
+        dt = time.perf_counter() - t0
+        kernel_s = e0.elapsed_time(e1) / 1e3
+        info = b.info()
+        end_hash, pop = b.hash(), b.population()
+        gens = steps * gps
+    return {
+        "metric": "cell updates/sec (GCUPS) of gol_step on the C-ABI board",
+        "value": round(W * H * gens / dt / 1e9, 3),
+        "unit": "GCUPS",
+        "n_gpus": 1,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / steps * 1e3, 4),
+        "us_per_generation": round(dt / gens * 1e6, 4),
+        "us_per_generation_kernel": round(kernel_s / gens * 1e6, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (bit-packed cells)" if info["packed"] else "u8 (byte cells)",
+        "data": f"synthetic ({args.init}, seed {args.seed})",
+        "config": {"workload": f"{W}x{H} {args.boundary} board, {args.init} seed {args.seed}, {gens} generations "
+                               f"timed in {steps} gol_step call(s)",
+                   "width": W, "height": H, "boundary": args.boundary, "init": args.init, "seed": args.seed,
+                   "generations_per_step": gps, "first_generation_timed": first, "generations_timed": gens,
+                   "tblock_k": info["tblock_k"], "interleave": info["ilv"], "parallelism": "single board",
+                   "initial_hash": f"{h0:016x}", "final_hash": f"{end_hash:016x}", "final_population": pop},
+        "hip_runtime": _lib_runtimes(),
+    }
+
+
+def _lib_runtimes():
+    from gameoflifewithactors_amd import _lib
+
+    return _lib.hip_runtimes()
 
 
 def main():
     args = parse()
+    if args.handle_leg_child:  # rank 0's child process (run_handle_leg)
+        import torch
+
+        from gameoflifewithactors_amd import TORUS, BOUNDED
+
+        boundary = TORUS if args.boundary == "torus" else BOUNDED
+        print(json.dumps(handle_leg(args, args.width, args.height, boundary, args.handle_parts,
+                                    torch.cuda.device_count())), flush=True)
+        return
+    if args.init != "splitmix":
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+            raise SystemExit("--init other than splitmix times the single C-ABI board (N = 1)")
+        import torch
+
+        torch.cuda.set_device(0)
+        print(json.dumps(board_leg(args)), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
@@ -213,13 +359,16 @@ def main():
     torch.cuda.set_device(dev)
     host_group = None
     if world > 1:
+        # a mis-paired exchange or a dead peer ends the run with an error after this long instead of hanging
+        timeout = datetime.timedelta(seconds=120)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev), timeout=timeout)
             # host-side barrier for the handle leg: the waiting ranks must not keep an RCCL kernel spinning
             # on the devices rank 0's one-process board is running on
-            host_group = dist.new_group(backend="gloo")
+            host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=max(
+                120, args.handle_timeout + 60)))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
             host_group = dist.group.WORLD
 
     from gameoflifewithactors_amd import TORUS, BOUNDED
@@ -279,6 +428,7 @@ def main():
         torch.cuda.synchronize()
 
     stream = runner.compute_stream
+    first_gen = runner.generation  # generations the board has advanced before the timed window (race + warmup)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
@@ -340,7 +490,9 @@ def main():
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     slots = valu_slots_per_word_gen(ilv)
     valu_tslots = slots * (cells_gpu / 32) * k / avg_launch_s / 1e12
-    tr = load_traffic(args.traffic_json, f"{W}x{args.height}_k{k}") or {}
+    fingerprint = _lib.device_code_fingerprint()
+    tkey = traffic_key(W, args.height, args.boundary, k, ilv)
+    tr = (load_traffic(args.traffic_json, tkey, fingerprint) or {}) if world == 1 else {}
     traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)
 
     # One-process C-ABI leg (rank 0), after the main leg; the other ranks wait on a host barrier.
@@ -351,10 +503,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier(group=host_group)
         if rank == 0:
-            try:
-                handle = handle_leg(args, W, H, boundary, parts, torch.cuda.device_count())
-            except Exception as e:  # reported, never fatal to the main line
-                handle = {"error": f"{type(e).__name__}: {e}"}
+            handle = run_handle_leg(args, W, H, boundary, parts, torch.cuda.device_count())
         if world > 1:
             dist.barrier(group=host_group)
 
@@ -380,6 +529,7 @@ def main():
                 "width": W,
                 "height": H,
                 "generations_per_step": k,
+                "first_generation_timed": first_gen,
                 "generations_timed": args.steps * k,
                 "tblock_autotune_us_per_gen": tune,
                 "interleave": ilv,
@@ -394,7 +544,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "traffic_source": "profiles/pmc_traffic.json (tools/pmc_traffic.sh)" if traffic else None,
+                "traffic_source": (f"profiles/pmc_traffic.json[{tkey}] (tools/pmc_traffic.sh), measured on this "
+                                   f"build's device code {fingerprint}") if traffic else
+                (f"no PMC measurement of {tkey} on this build's device code ({fingerprint})" if world == 1 else
+                 "PMC traffic is measured at N = 1 only"),
                 "kernel": f"gol_stream_step<K={k}, M={ilv}>",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
@@ -410,6 +563,8 @@ def main():
             "effective_hbm_gbs": round(cells * gens / dt * 0.25 / world / 1e9, 1),
             "roofline_k1_stream": k1,
             "hbm_copy_measured_gbs": copy_gbs,
+            "hip_runtime": _lib.hip_runtimes(),
+            "device_code": fingerprint,
         }
         if handle is not None:
             result["handle_leg"] = handle

@@ -20,6 +20,7 @@ GOL_ERR_NO_DEVICE = -5
 
 TORUS = 0
 BOUNDED = 1
+TRANSPORT_NONE, TRANSPORT_PEER, TRANSPORT_RCCL = 0, 1, 2
 INIT_DOTNET_MOD2 = 0
 INIT_DOTNET_NEXT2 = 1
 
@@ -34,6 +35,13 @@ _ERRORS = {
 
 class GolError(RuntimeError):
     pass
+
+
+class Xfer(ctypes.Structure):
+    """``gol_xfer`` (include/gol/gol.h): one halo message of a multi-part board's pass."""
+
+    _fields_ = [("part", ctypes.c_int32), ("op", ctypes.c_int32), ("peer", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("row", ctypes.c_int64), ("nrows", ctypes.c_int64)]
 
 
 class Strip(ctypes.Structure):
@@ -108,11 +116,74 @@ SIGNATURES = {
     "gol_strip_hash_partial": (ctypes.c_int, [sp, vp, vp, vp]),
     "gol_hash_finalize": (u64, [u64, i64, i64]),
     "gol_strip_plan": (ctypes.c_int, [sp, ctypes.c_int, i64, i64, i64p, i64p]),
+    "gol_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64]),
+    "gol_transport": (ctypes.c_int, [vp, ip, ctypes.c_char_p, i64]),
+    "gol_exchange_plan": (ctypes.c_int, [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, ctypes.POINTER(Xfer), i64,
+                                         i64p]),
+    "gol_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
 }
 
 
+def device_code_fingerprint(path: str = LIB_PATH) -> str | None:
+    """sha256 (first 16 hex digits) of the gfx950 device code in a built library: the ELF section `.hip_fatbin`,
+    which holds every kernel's code object.  PMC measurements (profiles/pmc_traffic.json) record it, and bench.py
+    uses a measurement only for the build it was taken on."""
+    import hashlib
+    import struct
+
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sec(i):
+        name, _type, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    return None
+
+
+def hip_runtimes() -> list:
+    """Paths of every HIP runtime (libamdhip64) mapped into this process (Linux /proc/self/maps)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and "libamdhip64" in os.path.basename(parts[-1]):
+                    paths.add(os.path.realpath(parts[-1]))
+    except OSError:
+        pass
+    return sorted(paths)
+
+
+def _torch_runtime_first() -> None:
+    """torch ships its own HIP runtime (torch/lib/libamdhip64.so, ROCm 7.0) under the same soname as the one
+    libgol_hip.so links (/opt/rocm/lib/libamdhip64.so.7, ROCm 7.2), and the dynamic loader binds every later
+    library to whichever was loaded first.  If libgol_hip.so came first, torch's own kernels ran on the 7.2
+    runtime and its lazy init failed ("No HIP GPUs are available", profiles/r2/pytest_parity_d.log).  So when
+    torch is importable it is imported BEFORE the library: the process then has one runtime, torch's, shared by
+    torch and libgol_hip.so.  A process without torch (the F# host, the C++ mirror) uses /opt/rocm's."""
+    try:
+        import torch  # noqa: F401  (loads torch's libamdhip64)
+    except Exception:  # torch absent or broken: the library brings its own runtime
+        pass
+
+
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libgol_hip.so; raises (never falls back) when it is absent."""
+    """Load libgol_hip.so; raises (never falls back) when it is absent.  Raises GolError when two HIP runtimes end
+    up mapped into the process (torch's and /opt/rocm's)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -121,13 +192,29 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             f"{path} not found: build it with `python -m gameoflifewithactors_amd.build` "
             "(there is no CPU fallback for the hot path)"
         )
+    _torch_runtime_first()
     lib = ctypes.CDLL(path)
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise GolError("two HIP runtimes are mapped into this process (" + ", ".join(rts) + "): torch and "
+                       "libgol_hip.so must share one; import torch before loading libgol_hip.so")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def exchange_plan(height: int, boundary: int, nparts: int, ghost: int, k: int) -> list:
+    """gol_exchange_plan: the halo messages of one pass of a multi-part board, in issue order per part:
+    [(part, "send"|"recv", peer, first buffer row, rows)].  Host-only."""
+    lib = load()
+    n = ctypes.c_int64()
+    check(lib.gol_exchange_plan(height, boundary, nparts, ghost, k, None, 0, ctypes.byref(n)), "gol_exchange_plan")
+    ops = (Xfer * n.value)()
+    check(lib.gol_exchange_plan(height, boundary, nparts, ghost, k, ops, n.value, ctypes.byref(n)), "gol_exchange_plan")
+    return [(x.part, "send" if x.op == 0 else "recv", x.peer, x.row, x.nrows) for x in ops]
 
 
 def check(rc: int, what: str = "") -> None:

@@ -4,7 +4,7 @@ Reference seam: ``cells : IDictionary<int*int, CellRef>`` built from ``createCel
 ``GameOfLife/GameOfLife/GameOfLifeDriver.fs:16-30`` (Akka: ``GameofLife.fs:148-163``).  One ``Board``
 holds the whole grid in HBM (bit-packed when the width is a multiple of 32) and ``step(1)`` is one
 ``updateView()`` tick (``GameOfLifeDriver.fs:32-34``) -- computed by the HIP kernels in
-``csrc/gol_kernels.hip`` through the C ABI in ``include/gol/gol.h``.
+``csrc/`` (streaming pass ``gol_step.hip``) through the C ABI in ``include/gol/gol.h``.
 """
 from __future__ import annotations
 
@@ -35,10 +35,11 @@ class Board:
               halo rows (``gol_create``; bit-identical to one GPU).
     devices: explicit strip placement (``gol_create_multi``), e.g. ``[0, 0, 0]`` runs three strips on one GPU.
     ilv: packed layout, words per interleaved block (0 = library default for the width; 1, 2, 4).
+    options: {name: value} passed to gol_set_option after creation (e.g. {"coop": 0}).
     """
 
     def __init__(self, width: int, height: int, boundary: int = TORUS, tblock_k: int = 0, num_gpus: int = 1,
-                 ilv: int = 0, devices=None):
+                 ilv: int = 0, devices=None, options: dict | None = None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
         if devices is not None:
@@ -50,6 +51,8 @@ class Board:
                   "gol_create")
         self._h = h
         self.width, self.height, self.boundary = width, height, boundary
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
 
     # ---------------------------------------------------------------- lifetime
     def close(self) -> None:
@@ -146,6 +149,17 @@ class Board:
         check(self._lib.gol_clear(self._h), "gol_clear")
         return self
 
+    # ---------------------------------------------------------------- options
+    def set_option(self, name: str, value: int) -> "Board":
+        """Per-board path / tuning option (gol_set_option, include/gol/gol.h lists the names)."""
+        check(self._lib.gol_set_option(self._h, name.encode(), int(value)), f"gol_set_option({name})")
+        return self
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(self._lib.gol_get_option(self._h, name.encode(), ctypes.byref(v)), f"gol_get_option({name})")
+        return v.value
+
     # ---------------------------------------------------------------- stepping
     def step(self, generations: int = 1) -> "Board":
         check(self._lib.gol_step(self._h, generations), "gol_step")
@@ -198,6 +212,13 @@ class Board:
                   "gol_part_info")
             out.append({"device": d.value, "y0": y0.value, "rows": rows.value, "ghost": ghost.value})
         return out
+
+    def transport(self) -> str:
+        """How the halo rows move (gol_transport): 'rccl: ...', 'peer: ...' or 'none: ...' with the reason."""
+        t = ctypes.c_int()
+        note = ctypes.create_string_buffer(512)
+        check(self._lib.gol_transport(self._h, ctypes.byref(t), note, len(note)), "gol_transport")
+        return {0: "none", 1: "peer", 2: "rccl"}[t.value] + ": " + note.value.decode(errors="replace")
 
     def pass_timing(self) -> list:
         """Advance one pass of the board's temporal depth with HIP timing events (gol_pass_timing); per row

@@ -139,13 +139,8 @@ bool valid_k(int k) {
 // Interleave for a packed board of this width (gol_layout.h).  Measured on MI355X at 65536^2
 // (profiles/r1/sweep_ilv.log, w12_sweep*.log): ilv 2 with K = 12 is the fastest configuration, ilv 4 needs 240 window
 // VGPRs at K = 8 (2 waves/SIMD) and wastes 1/9 of its lanes on a 65536-wide row, ilv 1 pays 4x the
-// funnel shifts.  GOL_ILV overrides (experiments); an override that does not divide the width is ignored.
+// funnel shifts.  gol_create_ex takes an explicit interleave (experiments).
 int pick_ilv(int64_t width) {
-    static const int env = [] {
-        const char* e = std::getenv("GOL_ILV");
-        return e ? std::atoi(e) : 0;
-    }();
-    if ((env == 1 || env == 2 || env == 4) && width % (32 * env) == 0) return env;
     if (width % 64 == 0) return 2;
     return 1;
 }
@@ -174,34 +169,21 @@ constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;
 // many cells and 8192 wide: 4096^2 0.81 vs 1.62 us/generation on the streaming pass, 2048^2 0.44 vs 1.48, 512^2
 // 0.50 vs 1.49 (profiles/r2/ab_coop_xh_u.log), 8192 x 4096 1.76 vs 2.95, 8192^2 2.16 vs 4.25, 4096 x 8192 1.01
 // vs 4.14 (coop_wide_u.log, coop_wide_s.log); below the LDS-resident cut-over too: 256^2 bounded 0.41 vs 0.92 on
-// the LDS-resident pass, 512 x 256 0.50 vs 1.22 (cut_resident_q.log).  GOL_COOP=0 disables it (the LDS-resident and
-// streaming passes then take these boards), GOL_COOP_MAX_CELLS moves the upper cut-over (A/B runs; read per call).
+// the LDS-resident pass, 512 x 256 0.50 vs 1.22 (cut_resident_q.log).  The board options "coop" (0 disables it:
+// the LDS-resident and streaming passes then take these boards) and "coop_max_cells" move the cut-over.
 constexpr int64_t kCoopMaxCells = (int64_t)1 << 26;
-bool coop_enabled() {
-    const char* e = std::getenv("GOL_COOP");
-    return !(e && e[0] == '0');
-}
 constexpr int kCoopFlagWords = 1024;            // bands of one launch at most (one per CU) ...
 constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
 constexpr int64_t kCoopMaxGensPerLaunch = 32768;  // a launch's granule tags count its blocks in 16 bits
 
-// Layout and depth a new board gets when the caller leaves them at 0.
-int board_ilv(int64_t width, int64_t height) {
-    const int env = pick_ilv(width);
-    if (std::getenv("GOL_ILV") != nullptr) return env;
+// Layout and depth a new board gets when the caller leaves them at 0.  nparts: row strips (devices) of the board.
+int board_ilv(int64_t width, int64_t height, int nparts) {
     const int64_t cells = width * height;
-    // boards the cooperative pass takes: its interleave, so a block costs 2 funnel shifts instead of 2 per word
+    // single boards the cooperative pass takes: its interleave, so a block costs 2 funnel shifts instead of 2 per
+    // word (a multi-GPU board never runs that pass: it keeps the streaming layout)
     const int m = width % 32 == 0 ? gol::coop_m(width / 32) : 0;
-    if (coop_enabled() && m > 1 && cells > kResidentMaxCells && cells <= kCoopMaxCells) return m;
-    return cells < kSmallBoardCells ? 1 : env;
-}
-// Boards up to this many cells run every gol_step call as ONE launch of the LDS-resident kernel
-// (gol_resident.hip) when the layout fits it: whole board in one workgroup's LDS, one barrier per
-// generation.  GOL_RESIDENT_MAX_CELLS overrides (0 disables; experiments and A/B runs).
-// Read on every call, so one process can A/B both paths (tests/test_gpu_resident.py).
-int64_t resident_max_cells(bool packed) {
-    const char* e = std::getenv("GOL_RESIDENT_MAX_CELLS");
-    return e ? (int64_t)std::atoll(e) : (packed ? kResidentMaxCells : kResidentBytesMaxCells);
+    if (nparts == 1 && m > 1 && cells > kResidentMaxCells && cells <= kCoopMaxCells) return m;
+    return cells < kSmallBoardCells ? 1 : pick_ilv(width);
 }
 
 int board_tblock(int ilv, int64_t cells, int boundary) {
@@ -219,8 +201,26 @@ namespace gol {
 int api_fail(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace gol
 
+// Per-board path and tuning options (gol_set_option).  The library reads no environment variable: a stray one in
+// the host process cannot change kernel paths.  Defaults are the measured ones.
+struct BoardOptions {
+    bool coop = true;                         // "coop": cooperative register-band pass for mid-size boards
+    int coop_k = 0;                           // "coop_k": generations per hand-off (0 = min(tblock_k, 8))
+    int64_t coop_max_cells = kCoopMaxCells;   // "coop_max_cells": largest board the cooperative pass takes
+    int64_t resident_max_cells = -1;          // "resident_max_cells": LDS-resident cut-over (-1 = per layout)
+    bool wave_resident = true;                // "wave_resident": single-wave pass for boards <= 128 x 256
+    int32_t split = 0;                        // "split": streaming pair split, 1/65536 (0 = engine, < 0 = off)
+    int64_t seg_rows = 0;                     // "seg_rows": streaming rows per wave segment (0 = planned)
+    int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
+    int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
+    int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
+    int resident_threads = 1024;              // "resident_threads": LDS-resident workgroup size (1024 or 256)
+};
+
 struct gol_board {
     std::mutex mu;
+    BoardOptions opt;
+    bool invalid = false;  // a cooperative hand-off timed out: readbacks fail until the board is overwritten
     int device = 0;
     hipStream_t stream = nullptr;
     int64_t W = 0, H = 0;
@@ -257,6 +257,8 @@ struct gol_board {
         a.out_end = out_end;
         a.seg = 0;
         a.ilv = ilv;
+        a.split_opt = opt.split;
+        a.seg_opt = opt.seg_rows;
         return a;
     }
 };
@@ -270,16 +272,36 @@ int check_board(gol_board* b) {
     return GOL_OK;
 }
 
+// After the board's stream has drained: a cooperative pass whose hand-off wait timed out left a wrong board.  Its
+// error word is read (and cleared) here, after every synchronisation a caller can observe -- gol_synchronize and
+// every readback -- and the board stays invalid until it is overwritten (set_cells, load, seed, clear).
+int check_valid(gol_board* b) {
+    if (b->coop) {
+        int err = 0;
+        GOL_HIP(hipMemcpyAsync(&err, b->coop + kCoopErrWord, sizeof(int), hipMemcpyDeviceToHost, b->stream));
+        GOL_HIP(hipStreamSynchronize(b->stream));
+        if (err) {
+            b->invalid = true;
+            GOL_HIP(hipMemsetAsync(b->coop + kCoopErrWord, 0, sizeof(unsigned), b->stream));
+            GOL_HIP(hipStreamSynchronize(b->stream));
+        }
+    }
+    if (b->invalid)
+        return fail(GOL_ERR_HIP, "cooperative pass: a band hand-off timed out (were other kernels occupying CUs?); "
+                                 "the board is invalid until it is overwritten (set_cells, load, seed, clear)");
+    return GOL_OK;
+}
+
 int sync(gol_board* b) {
     if (b->multi) return b->multi->synchronize();
     GOL_HIP(hipStreamSynchronize(b->stream));
-    if (b->coop) {  // a cooperative pass whose neighbour wait timed out left a wrong board: report it
-        int err = 0;
-        GOL_HIP(hipMemcpy(&err, b->coop + kCoopErrWord, sizeof(int), hipMemcpyDeviceToHost));
-        if (err) return fail(GOL_ERR_HIP, "cooperative pass: a band hand-off timed out (were other kernels "
-                                          "occupying CUs?); the board is invalid");
-    }
-    return GOL_OK;
+    return check_valid(b);
+}
+
+// The board's cells were replaced as a whole: a timed-out hand-off no longer matters.
+int overwritten(gol_board* b) {
+    b->invalid = false;
+    return sync(b);
 }
 
 int set_cells_impl(gol_board* b, const uint8_t* host) {
@@ -287,7 +309,7 @@ int set_cells_impl(gol_board* b, const uint8_t* host) {
     const size_t n = (size_t)(b->W * b->H);
     if (!b->packed) {
         GOL_HIP(hipMemcpyAsync(b->cells(b->cur), host, n, hipMemcpyHostToDevice, b->stream));
-        return sync(b);
+        return overwritten(b);
     }
     uint8_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, n);
@@ -302,7 +324,7 @@ int set_cells_impl(gol_board* b, const uint8_t* host) {
     } while (0);
     if (e != hipSuccess) rc = fail(GOL_ERR_HIP, std::string("set_cells: ") + hipGetErrorString(e));
     (void)hipFree(staging);
-    return rc;
+    return rc == GOL_OK ? overwritten(b) : rc;
 }
 
 int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
@@ -329,7 +351,7 @@ int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
     } while (0);
     if (e != hipSuccess) rc = fail(GOL_ERR_HIP, std::string("readback: ") + hipGetErrorString(e));
     (void)hipFree(staging);
-    return rc;
+    return rc == GOL_OK ? check_valid(b) : rc;
 }
 
 int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
@@ -349,33 +371,39 @@ int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
     unsigned long long v = 0;
     GOL_HIP(hipMemcpyAsync(&v, b->acc, sizeof(v), hipMemcpyDeviceToHost, b->stream));
     GOL_HIP(hipStreamSynchronize(b->stream));
+    if (int rc = check_valid(b)) return rc;
     *out = hash ? gol_hash_finalize(v, b->W, b->H) : (uint64_t)v;
     return GOL_OK;
 }
 
+// Boards up to this many cells run every gol_step call as ONE launch of the LDS-resident kernel
+// (gol_resident.hip) when the layout fits it: whole board in one workgroup's LDS, one barrier per
+// generation.  The board option "resident_max_cells" overrides (0 disables; tests/test_gpu_resident.py).
+int64_t resident_max_cells(const gol_board* b) {
+    if (b->opt.resident_max_cells >= 0) return b->opt.resident_max_cells;
+    return b->packed ? kResidentMaxCells : kResidentBytesMaxCells;
+}
+
 // Boards small enough for one wavefront's registers (gol_wave.hip: W <= 128, H <= 256) run every gol_step call
-// as one single-wave launch; GOL_WAVE_RESIDENT=0 disables it (A/B runs), read on every call.
+// as one single-wave launch (board option "wave_resident" = 0 disables it).
 bool use_wave_resident(const gol_board* b) {
-    const char* e = std::getenv("GOL_WAVE_RESIDENT");
-    if (e && e[0] == '0') return false;
+    if (!b->opt.wave_resident) return false;
     return gol::wave_resident_rpl(b->W, b->H) > 0 && (!b->packed || b->ilv == 1);
 }
 
-// Generations per hand-off of the cooperative pass: GOL_COOP_K if set (A/B runs), else the board's
-// temporal-block cap, at most gol::coop_k().
+// Generations per hand-off of the cooperative pass: the board's "coop_k" option if set, else its temporal-block
+// cap, at most gol::kCoopDefaultK.
 int coop_depth(const gol_board* b) {
-    if (std::getenv("GOL_COOP_K")) return gol::coop_k();
-    return b->tblock < gol::coop_k() ? b->tblock : gol::coop_k();
+    if (b->opt.coop_k > 0) return b->opt.coop_k;
+    return b->tblock < gol::kCoopDefaultK ? b->tblock : gol::kCoopDefaultK;
 }
 
 bool use_coop(const gol_board* b) {
-    if (!coop_enabled() || !b->packed) return false;
-    const char* m = std::getenv("GOL_COOP_MAX_CELLS");
-    const int64_t maxc = m ? (int64_t)std::atoll(m) : kCoopMaxCells;
+    if (!b->opt.coop || !b->packed) return false;
     const int cm = gol::coop_m(b->W / 32);
     int nwg = 0, B = 0, R = 0;
-    return (b->ilv == 1 || b->ilv == cm) && b->W * b->H <= maxc &&
-           gol::coop_plan(b->W, b->H, coop_depth(b), &nwg, &B, &R) && nwg < kCoopFlagWords;
+    return (b->ilv == 1 || b->ilv == cm) && b->W * b->H <= b->opt.coop_max_cells &&
+           gol::coop_plan(b->W, b->H, coop_depth(b), &nwg, &B, &R, b->opt.coop_r) && nwg < kCoopFlagWords;
 }
 
 // Words per lane of the cooperative pass for a ragged row of nw words (rows padded to a multiple of it).
@@ -387,15 +415,14 @@ int coop_m_ragged(int64_t nw) { return nw <= 64 ? 1 : (nw <= 128 ? 2 : (nw <= 25
 // generations' worth.
 constexpr int64_t kCoopRaggedMinGens = 16;
 bool use_coop_ragged(const gol_board* b, int64_t* pitch) {
-    if (!coop_enabled() || b->packed || b->W % 32 == 0) return false;
-    const char* m = std::getenv("GOL_COOP_MAX_CELLS");
-    const int64_t maxc = m ? (int64_t)std::atoll(m) : kCoopMaxCells;
+    if (!b->opt.coop || b->packed || b->W % 32 == 0) return false;
     const int64_t nw = (b->W + 31) / 32;
     const int cm = coop_m_ragged(nw);
-    if (!cm || b->W * b->H > maxc) return false;
+    if (!cm || b->W * b->H > b->opt.coop_max_cells) return false;
     const int64_t nwp = (nw + cm - 1) / cm * cm;
     int nwg = 0, B = 0, R = 0;
-    if (!gol::coop_plan(nwp * 32, b->H, coop_depth(b), &nwg, &B, &R) || nwg >= kCoopFlagWords) return false;
+    if (!gol::coop_plan(nwp * 32, b->H, coop_depth(b), &nwg, &B, &R, b->opt.coop_r) || nwg >= kCoopFlagWords)
+        return false;
     *pitch = nwp;
     return true;
 }
@@ -411,7 +438,7 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     }
     int nwg = 0, B = 0, R = 0;
     const int k = coop_depth(b);
-    (void)gol::coop_plan(W, b->H, k, &nwg, &B, &R);
+    (void)gol::coop_plan(W, b->H, k, &nwg, &B, &R, b->opt.coop_r);
     const int64_t need = gol::coop_xch_words(W, nwg, k);
     if (need > b->coop_xch_words) {
         if (b->coop_xch) {
@@ -423,10 +450,11 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
         GOL_HIP(hipMalloc(&b->coop_xch, (size_t)need * sizeof(uint32_t)));
         b->coop_xch_words = need;
         b->coop_epoch = 0xffff;  // forces the clear below: a fresh buffer holds arbitrary tags
-    } else if (const char* e0 = std::getenv("GOL_COOP_EPOCH")) {
-        // tests: the next launch's epoch (runs the 16-bit wrap, and the clear of the granules it needs, early)
-        b->coop_epoch = (unsigned)std::atoi(e0) & 0xffffu;
     }
+    gol::CoopTuning tune;
+    tune.min_rows = b->opt.coop_r;
+    tune.poll_delay = b->opt.coop_poll_delay;
+    tune.spin_limit = (unsigned)std::min<int64_t>(b->opt.coop_spin_limit, 0xffffffffLL);
     while (gens > 0) {
         const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;
         if (++b->coop_epoch > 0xffff) {  // tags of an earlier epoch could match again: clear the granules
@@ -435,7 +463,7 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
         }
         GOL_HIP(gol::launch_coop_pass(bufs[*cur], bufs[*cur ^ 1], W, b->H, pitch, ilv, k, g, b->boundary == GOL_BOUNDED,
                                       b->coop_epoch, reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
-                                      b->coop_xch_words, b->stream, ragged_w));
+                                      b->coop_xch_words, b->stream, ragged_w, tune));
         *cur ^= 1;
         b->generation += g;
         gens -= g;
@@ -481,7 +509,7 @@ int step_impl(gol_board* b, int64_t gens) {
         b->cur ^= 1;
         return GOL_OK;
     }
-    if (gens > 0 && b->W * b->H <= resident_max_cells(b->packed) &&
+    if (gens > 0 && b->W * b->H <= resident_max_cells(b) &&
         (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
         const bool bounded = b->boundary == GOL_BOUNDED;
         while (gens > 0) {
@@ -490,10 +518,10 @@ int step_impl(gol_board* b, int64_t gens) {
             const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
             if (b->packed)
                 GOL_HIP(gol::launch_resident_packed(b->words(b->cur), b->words(b->cur ^ 1), b->W, b->H, b->pitch, g,
-                                                    bounded, b->stream));
+                                                    bounded, b->stream, b->opt.resident_threads));
             else
                 GOL_HIP(gol::launch_resident_bytes(b->cells(b->cur), b->cells(b->cur ^ 1), b->W, b->H, g, bounded,
-                                                   b->stream));
+                                                   b->stream, b->opt.resident_threads));
             b->cur ^= 1;
             b->generation += g;
             gens -= g;
@@ -644,7 +672,7 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->boundary = boundary;
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
-        b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height)) : 0;
+        b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n)) : 0;
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = devices ? hipSetDevice(devices[0]) : hipSuccess;
@@ -754,6 +782,41 @@ int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* row
     return GOL_OK;
 }
 
+int gol_transport(gol_board* b, int* transport, char* note, int64_t note_len) {
+    if (!b || !transport) return fail(GOL_ERR_INVALID, "null argument");
+    std::string n = "single board: no halo exchange";
+    *transport = GOL_TRANSPORT_NONE;
+    if (b->multi) {
+        *transport = b->multi->transport();
+        n = b->multi->transport_note();
+    }
+    if (note && note_len > 0) {
+        const size_t len = std::min<size_t>(n.size(), (size_t)note_len - 1);
+        std::memcpy(note, n.data(), len);
+        note[len] = '\0';
+    }
+    return GOL_OK;
+}
+
+int gol_exchange_plan(int64_t height, int boundary, int nparts, int64_t ghost, int k, gol_xfer* ops, int64_t max_ops,
+                      int64_t* n_ops) {
+    if (!n_ops || nparts < 2 || height < nparts || k < 1 || ghost < k || (boundary != GOL_TORUS && boundary != GOL_BOUNDED))
+        return fail(GOL_ERR_INVALID, "bad exchange plan arguments (nparts >= 2, height >= nparts, ghost >= k >= 1)");
+    for (int r = 0; r < nparts; r++)
+        if (height * (r + 1) / nparts - height * r / nparts < k) return fail(GOL_ERR_INVALID, "a part is thinner than k");
+    try {
+        const std::vector<gol_xfer> plan = gol::exchange_plan(height, boundary, nparts, ghost, k);
+        *n_ops = (int64_t)plan.size();
+        if (ops) {
+            if (max_ops < (int64_t)plan.size()) return fail(GOL_ERR_INVALID, "ops array too small");
+            std::copy(plan.begin(), plan.end(), ops);
+        }
+    } catch (const std::exception& ex) {
+        return fail(GOL_ERR_OOM, ex.what());
+    }
+    return GOL_OK;
+}
+
 int gol_destroy(gol_board* b) {
     if (!b) return fail(GOL_ERR_INVALID, "null board");
     DeviceGuard dg(b->device);
@@ -801,7 +864,7 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
     } while (0);
     (void)hipFree(staging);
     if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("get_region: ") + hipGetErrorString(e));
-    return GOL_OK;
+    return check_valid(b);
 }
 
 int gol_render_gray8(gol_board* b, uint8_t* pixels, int64_t stride, uint8_t alive_value) {
@@ -833,7 +896,7 @@ int gol_save_packed(gol_board* b, uint64_t* words, int64_t len) {
     } while (0);
     (void)hipFree(staging);
     if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("save_packed: ") + hipGetErrorString(e));
-    return GOL_OK;
+    return check_valid(b);
 }
 
 int gol_load_packed(gol_board* b, const uint64_t* words, int64_t len) {
@@ -858,7 +921,7 @@ int gol_load_packed(gol_board* b, const uint64_t* words, int64_t len) {
     } while (0);
     (void)hipFree(staging);
     if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("load_packed: ") + hipGetErrorString(e));
-    return GOL_OK;
+    return overwritten(b);
 }
 
 int gol_seed_dotnet(gol_board* b, int32_t seed, int mode) {
@@ -894,7 +957,7 @@ int gol_seed_splitmix(gol_board* b, uint64_t seed) {
     else
         GOL_HIP(gol::launch_splitmix_bytes(b->cells(b->cur), b->W, b->H, seed, b->stream));
     b->generation = 0;
-    return sync(b);
+    return overwritten(b);
 }
 
 int gol_clear(gol_board* b) {
@@ -907,7 +970,7 @@ int gol_clear(gol_board* b) {
     }
     GOL_HIP(hipMemsetAsync(b->buf[b->cur], 0, b->bytes(), b->stream));
     b->generation = 0;
-    return sync(b);
+    return overwritten(b);
 }
 
 int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y) {
@@ -1010,6 +1073,12 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
         return fail(GOL_ERR_INVALID, "n must equal gol_num_parts and the arrays must be non-null");
     if (b->multi) return b->multi->timed_pass(interior_us, wait_us, edge_us, &b->generation);
     if (!b->packed) return fail(GOL_ERR_UNSUPPORTED, "pass timing needs a bit-packed board");
+    // a single board's timed pass is one streaming pass: boards whose gol_step takes another pass are refused, so
+    // the figure always describes the pass the board runs
+    if (use_wave_resident(b) || use_coop(b) ||
+        (b->W * b->H <= resident_max_cells(b) && b->ilv == 1 && gol::resident_packed_fits(b->W, b->H)))
+        return fail(GOL_ERR_UNSUPPORTED, "pass timing: this board's gol_step runs the single-wave, cooperative or "
+                                         "LDS-resident pass, not the streaming pass the timing measures");
     hipEvent_t e0 = nullptr, e1 = nullptr;
     GOL_HIP(hipEventCreate(&e0));
     hipError_t e = hipEventCreate(&e1);
@@ -1032,6 +1101,66 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
     interior_us[0] = 1e3 * ms;
     wait_us[0] = 0;
     edge_us[0] = 1e3 * ms;
+    return GOL_OK;
+}
+
+int gol_set_option(gol_board* b, const char* name, int64_t value) {
+    if (int rc = check_board(b)) return rc;
+    if (!name) return fail(GOL_ERR_INVALID, "null option name");
+    std::lock_guard<std::mutex> g(b->mu);
+    const std::string n(name);
+    BoardOptions& o = b->opt;
+    if (n == "coop") o.coop = value != 0;
+    else if (n == "coop_k") {
+        if (value < 0 || value > 64) return fail(GOL_ERR_INVALID, "coop_k must be 0 (default) .. 64");
+        o.coop_k = (int)value;
+    } else if (n == "coop_max_cells") o.coop_max_cells = value;
+    else if (n == "resident_max_cells") o.resident_max_cells = value;
+    else if (n == "wave_resident") o.wave_resident = value != 0;
+    else if (n == "split") {
+        if (value >= 65536) return fail(GOL_ERR_INVALID, "split must be < 65536 (1/65536 units; 0 default, < 0 off)");
+        o.split = (int32_t)(value < 0 ? -1 : value);
+    } else if (n == "seg_rows") o.seg_rows = value < 0 ? 0 : value;
+    else if (n == "coop_r") {
+        if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
+        o.coop_r = (int)value;
+    } else if (n == "coop_poll_delay") {
+        if (value < 0 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be 0..4096");
+        o.coop_poll_delay = (int)value;
+    } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
+    else if (n == "resident_threads") {
+        if (value != 256 && value != 1024) return fail(GOL_ERR_INVALID, "resident_threads must be 256 or 1024");
+        o.resident_threads = (int)value;
+    } else if (n == "coop_epoch") {
+        // the epoch of the last cooperative launch, so the next one runs at value + 1: tests run the 16-bit wrap
+        // (and the clear of the granules it needs) early.  Only meaningful once the exchange buffer exists.
+        if (value < 0 || value > 0xffff) return fail(GOL_ERR_INVALID, "coop_epoch must be 0..65535");
+        if (b->coop_xch) b->coop_epoch = (unsigned)value;
+    } else
+        return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
+    return GOL_OK;
+}
+
+int gol_get_option(gol_board* b, const char* name, int64_t* value) {
+    if (int rc = check_board(b)) return rc;
+    if (!name || !value) return fail(GOL_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(b->mu);
+    const std::string n(name);
+    const BoardOptions& o = b->opt;
+    if (n == "coop") *value = o.coop;
+    else if (n == "coop_k") *value = o.coop_k;
+    else if (n == "coop_max_cells") *value = o.coop_max_cells;
+    else if (n == "resident_max_cells") *value = o.resident_max_cells;
+    else if (n == "wave_resident") *value = o.wave_resident;
+    else if (n == "split") *value = o.split;
+    else if (n == "seg_rows") *value = o.seg_rows;
+    else if (n == "coop_r") *value = o.coop_r;
+    else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
+    else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
+    else if (n == "resident_threads") *value = o.resident_threads;
+    else if (n == "coop_epoch") *value = b->coop_epoch;
+    else
+        return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
     return GOL_OK;
 }
 

@@ -40,7 +40,7 @@ namespace {
 constexpr int kWaves = 16;                 // waves per workgroup: 4 per SIMD
 constexpr int kThreads = 64 * kWaves;
 constexpr int kMinLds = 96 * 1024;         // > half the CU's 160 KiB: one workgroup per CU
-constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident
+constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident (default)
 // The wave-edge exchange per generation carries the edge rows' horizontal sums (1) or the raw rows (0, A/B)
 #ifndef GOL_COOP_XH
 #define GOL_COOP_XH 1
@@ -64,6 +64,7 @@ struct CoopArgs {
     int gens;
     unsigned epoch;       // launch epoch (16 bits) of the granule tags
     int poll_delay;       // s_sleep 1 periods (64 clocks) before the first poll of a hand-off
+    unsigned spin_limit;  // polls before a wait gives up (kSpinLimit unless a test lowers it)
     int* err;             // set to 1 by a timed-out wait
     int rag_lb;           // ragged rows (kLayRagged): bit of the last cell in the last word, (W - 1) & 31
     int rag_last;         // ragged rows: index of the last word that holds cells, ceil(W / 32) - 1
@@ -86,7 +87,7 @@ __device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M],
 // row pair) ran slower batched (8192 x 4096 1.69 vs 1.61) and poll granule by granule, at once.
 template <int M, int R>
 __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uint32_t (&w)[R][M], unsigned tag,
-                                            int delay) {
+                                            int delay, unsigned spin_limit) {
     if constexpr (M >= 4) {
         bool ok = true;
 #pragma unroll
@@ -95,8 +96,8 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 uint64_t g = __hip_atomic_load(src[i] + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (unsigned it = 0; (unsigned)(g >> 32) != tag; it++) {
-                    if (it == kSpinLimit) {
+                for (unsigned it = 0; ok && (unsigned)(g >> 32) != tag; it++) {  // after a timeout: no more waits
+                    if (it == spin_limit) {
                         ok = false;
                         break;
                     }
@@ -123,7 +124,7 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
 #pragma unroll
             for (int t = 0; t < M; t++) miss = miss || (unsigned)(v[i][t] >> 32) != tag;
         if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
-        if (it == kSpinLimit) return false;
+        if (it == spin_limit) return false;
         __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     }  // ordered before their first read by the first generation's barrier
 
     const int nblk = (a.gens + K - 1) / K;
+    bool failed = false;  // wave-uniform: a hand-off wait of this launch timed out
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
         if (blk > 0) {
@@ -296,8 +298,18 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             bool any = false;
 #pragma unroll
             for (int i = 0; i < R; i++) any = any || src[i] != nullptr;
-            if (__builtin_amdgcn_ballot_w64(any) != 0 && !ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay))
+            // Once any wave of the launch has timed out (this one, or another band's: the error word, read by every
+            // lane and agreed by ballot, so it stays a vector load) the board is invalid: stop waiting, so a launch
+            // with a non-resident band ends after about one spin limit instead of one per block.  No early exit:
+            // every wave still meets the generation barriers.
+            if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
+                failed = true;
+            if (!failed && __builtin_amdgcn_ballot_w64(any) != 0 &&
+                !ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit)) {
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                failed = true;
+            }
         }
         // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j).  The wave's own row
         // sums do not depend on the exchange: they are summed between publishing the edge rows and the barrier,
@@ -476,27 +488,16 @@ const void* kernel_m(int r, int lay, bool bounded, bool full) {
 
 }  // namespace
 
-// Generations per block (the board's tblock_k caps it): GOL_COOP_K overrides (A/B), default 8.
-int coop_k() {
-    const char* e = std::getenv("GOL_COOP_K");
-    const int k = e ? std::atoi(e) : 8;
-    return k >= 1 && k <= 64 ? k : 8;
-}
-
 // Words per lane for a row of nw words (0: the width does not fit one wave).
 int coop_m(int64_t nw) {
     const int m = nw <= 64 ? 1 : (nw <= 128 ? 2 : 4);
     return nw <= 256 && nw % m == 0 ? m : 0;
 }
 
-// Rows per wave at least: GOL_COOP_R (A/B; fewer, taller wave slices re-sum fewer neighbour rows), default 1.
-static int coop_min_rows() {
-    const char* e = std::getenv("GOL_COOP_R");
-    const int r = e ? std::atoi(e) : 1;
-    return r >= 1 && r <= 8 ? r : 1;
-}
-
-bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R) {
+// min_rows: rows per wave at least (the board's "coop_r" option, A/B: fewer, taller wave slices re-sum fewer
+// neighbour rows; 1 by default).
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R, int min_rows) {
+    if (min_rows < 1 || min_rows > 8) min_rows = 1;
     const int cus = coop_cus();
     if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1 || !coop_m(W / 32)) return false;
     // balanced bands of >= k rows each (a k-row halo then comes from ONE neighbour band), one per CU at most
@@ -504,7 +505,7 @@ bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R) {
     if (n < 1) return false;
     const int64_t b = (H + n - 1) / n;  // the largest band
     int64_t rows = (b + 2 * k + kWaves - 1) / kWaves;  // rows per wave
-    if (rows < coop_min_rows()) rows = coop_min_rows();
+    if (rows < min_rows) rows = min_rows;
     int r = 0;
     for (int c : kRows)
         if (c >= rows) {
@@ -522,9 +523,9 @@ int64_t coop_xch_words(int64_t W, int nwg, int k) { return (int64_t)2 * 2 * nwg 
 
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
-                            hipStream_t s, int64_t ragged_w) {
+                            hipStream_t s, int64_t ragged_w, const CoopTuning& tune) {
     int nwg = 0, B = 0, R = 0;
-    if (!coop_plan(W, H, k, &nwg, &B, &R) || gens < 1 || gens > 65535 || pitch < W / 32 ||
+    if (!coop_plan(W, H, k, &nwg, &B, &R, tune.min_rows) || gens < 1 || gens > 65535 || pitch < W / 32 ||
         coop_xch_words(W, nwg, k) > xch_words)
         return hipErrorInvalidValue;
     const int nw = (int)(W / 32);
@@ -547,13 +548,8 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     a.err = err;
     a.rag_lb = ragged_w ? (int)((ragged_w - 1) & 31) : 31;
     a.rag_last = ragged_w ? (int)((ragged_w + 31) / 32 - 1) : nw - 1;
-    {  // s_sleep periods before the first poll of a hand-off (M <= 2; ld_granules); GOL_COOP_POLL_DELAY for A/B
-        static const int env = [] {
-            const char* e = std::getenv("GOL_COOP_POLL_DELAY");
-            return e ? std::atoi(e) : -1;
-        }();
-        a.poll_delay = env >= 0 ? env : 8;
-    }
+    a.poll_delay = tune.poll_delay >= 0 ? tune.poll_delay : 8;  // s_sleep periods before a first poll (ld_granules)
+    a.spin_limit = tune.spin_limit ? tune.spin_limit : kSpinLimit;
     const bool full = a.nl == 64;
     const int lay = ragged_w ? kLayRagged : (ilv == M && M > 1 ? kLayInterleaved : kLayWords);
     const void* fn = M == 1 ? kernel_m<1>(R, lay, bounded, full)

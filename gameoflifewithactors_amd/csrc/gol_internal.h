@@ -22,6 +22,8 @@ struct StreamArgs {
     int32_t split;      // filled by plan_stream: pair split (older wave's share of a pair segment, 1/65536;
                         // 0 = one segment per wave)
     int32_t spare;      // waves to leave free for concurrent launches (plan_stream)
+    int32_t split_opt;  // 0: the engine's pair split; > 0: this split (1/65536); < 0: none (board option "split")
+    int64_t seg_opt;    // 0: plan the segment length; > 0: rows per segment (board option "seg_rows")
 };
 
 // ---- gol_step.hip
@@ -71,23 +73,32 @@ hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, con
 // ---- gol_resident.hip: whole board in one workgroup's LDS, all generations in one launch
 bool resident_packed_fits(int64_t W, int64_t H);  // ilv = 1 layout
 bool resident_bytes_fits(int64_t W, int64_t H);
+// threads: 1024 (default) or 256 (board option "resident_threads")
 hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch,
-                                  int64_t gens, bool bounded, hipStream_t s);
+                                  int64_t gens, bool bounded, hipStream_t s, int threads = 1024);
 hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, int64_t gens, bool bounded,
-                                 hipStream_t s);
+                                 hipStream_t s, int threads = 1024);
 
 // ---- gol_coop.hip: one workgroup per CU owning a band of rows in registers, k generations per neighbour
 // hand-off (boards up to 8192 wide, ilv 1 or ilv = coop_m); the result lands in dst
-int coop_k();
+constexpr int kCoopDefaultK = 8;  // generations per hand-off unless the board's "coop_k" option or tblock_k says less
 int coop_m(int64_t nw);  // words per lane for rows of nw words (0: too wide for the pass)
-bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R);
+// min_rows: rows per wave at least (board option "coop_r", 1 by default)
+bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R, int min_rows = 1);
 int64_t coop_xch_words(int64_t W, int nwg, int k);  // exchange buffer the pass needs
 // gens <= 65535 per launch; epoch (1..65535) tags this launch's hand-off granules (clear xch before reusing one).
 // ragged_w > 0: a ragged board (width ragged_w, not a multiple of 32) packed into whole-word scratch rows of W cells
 // (launch_pack_ragged), ilv 1; 0: a packed board of width W.
+// poll_delay: s_sleep 1 periods before a hand-off's first poll (8); spin_limit: polls before a wait gives up and
+// sets *err (0 = the default, ~2 s); min_rows as for coop_plan.
+struct CoopTuning {
+    int min_rows = 1;
+    int poll_delay = 8;
+    unsigned spin_limit = 0;
+};
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
-                            hipStream_t s, int64_t ragged_w = 0);
+                            hipStream_t s, int64_t ragged_w = 0, const CoopTuning& tune = CoopTuning());
 
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
 int wave_resident_rpl(int64_t W, int64_t H);  // rows per lane, 0 = the board does not fit

@@ -3,9 +3,13 @@
 // Replaces, for a board too large or too slow for one GPU, the same reference seam as the single board:
 // the dictionary of cell actors built by GameOfLifeDriver.fs:16-30 and ticked by updateView (L32-34).
 // The per-pass protocol (ghost rows of depth k, interior || exchange, then the edge bands) is the one the
-// one-process-per-GPU path runs over RCCL (strips.py); here the exchange is a peer copy between devices
-// of the same process, ordered by HIP events instead of a communicator.
+// one-process-per-GPU path runs over torch.distributed (strips.py).  Here one process drives every part: the
+// exchange is RCCL send/recv over a communicator spanning the parts' devices (ncclCommInitAll) when every part
+// has its own GPU, or a peer copy ordered by HIP events when a device repeats (the one-GPU rehearsal).
 #include "gol_multi.h"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 
@@ -42,7 +46,84 @@ struct Staging {
     }
 };
 
+// RCCL, resolved at run time (dlopen): a process that never builds a multi-GPU board does not need librccl, and a
+// process that already loaded one (torch bundles its own under the same soname) shares it instead of loading a
+// second copy.
+struct Rccl {
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string error;  // why it is unavailable
+
+    static const Rccl& get() {
+        static const Rccl r = [] {
+            Rccl x;
+            void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+            if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+            if (!h) {
+                const char* e = dlerror();
+                x.error = std::string("dlopen librccl.so.1: ") + (e ? e : "?");
+                return x;
+            }
+            x.init_all = (decltype(x.init_all))dlsym(h, "ncclCommInitAll");
+            x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+            x.send = (decltype(x.send))dlsym(h, "ncclSend");
+            x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+            x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+            x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+            x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+            if (!x.init_all || !x.destroy || !x.send || !x.recv || !x.group_start || !x.group_end || !x.error_string)
+                x.error = "librccl.so.1 lacks a symbol of the send/recv API";
+            return x;
+        }();
+        return r;
+    }
+    bool ok() const { return error.empty(); }
+    std::string why(ncclResult_t r) const { return error_string ? error_string(r) : "rccl error"; }
+};
+
 }  // namespace
+
+std::vector<gol_xfer> exchange_plan(int64_t height, int boundary, int nparts, int64_t ghost, int k) {
+    std::vector<gol_xfer> ops;
+    const bool torus = boundary == GOL_TORUS;
+    for (int r = 0; r < nparts; r++) {
+        const int64_t rows = height * (r + 1) / nparts - height * r / nparts;
+        const int up = r > 0 ? r - 1 : (torus ? nparts - 1 : -1);
+        const int down = r < nparts - 1 ? r + 1 : (torus ? 0 : -1);
+        auto add = [&](int op, int peer, int64_t row) { ops.push_back(gol_xfer{r, op, peer, 0, row, k}); };
+        if (up >= 0) add(0, up, ghost);                        // my top k owned rows -> up's bottom ghost
+        if (down >= 0) add(0, down, ghost + rows - k);         // my bottom k owned rows -> down's top ghost
+        if (down >= 0) add(1, down, ghost + rows);             // down's top rows -> my bottom ghost
+        if (up >= 0) add(1, up, ghost - k);                    // up's bottom rows -> my top ghost
+    }
+    return ops;
+}
+
+int MultiBoard::init_rccl() {
+    const Rccl& nc = Rccl::get();
+    if (!nc.ok()) {
+        transport_note_ = "peer copies: " + nc.error;
+        return GOL_OK;
+    }
+    std::vector<int> devs;
+    for (const Part& p : parts_) devs.push_back(p.device);
+    std::vector<ncclComm_t> comms(parts_.size(), nullptr);
+    const ncclResult_t r = nc.init_all(comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) {
+        transport_note_ = "peer copies: ncclCommInitAll failed: " + nc.why(r);
+        return GOL_OK;
+    }
+    for (size_t i = 0; i < parts_.size(); i++) parts_[i].comm = comms[i];
+    rccl_ = true;
+    transport_note_ = "RCCL ncclSend/ncclRecv over one communicator per part (ncclCommInitAll, " +
+                      std::to_string(parts_.size()) + " devices)";
+    return GOL_OK;
+}
 
 int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock, int ilv) {
     W_ = width;
@@ -92,6 +173,18 @@ int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* dev
         }
         GOL_MHIP(hipMalloc(&p.acc, 64));
     }
+    // RCCL when every part has its own device; peer copies when a device repeats (RCCL refuses two ranks on one GPU)
+    std::vector<int> seen;
+    bool distinct = true;
+    for (const Part& p : parts_) {
+        if (std::find(seen.begin(), seen.end(), p.device) != seen.end()) distinct = false;
+        seen.push_back(p.device);
+    }
+    if (distinct) {
+        GOL_MRC(init_rccl());
+    } else {
+        transport_note_ = "peer copies: a device holds more than one part (RCCL needs one rank per GPU)";
+    }
     // peer access between neighbouring parts on distinct devices (xGMI); without it the copies are staged
     for (const Part& p : parts_)
         for (int q : {p.up, p.down}) {
@@ -113,6 +206,7 @@ MultiBoard::~MultiBoard() {
         if (hipSetDevice(p.device) != hipSuccess) continue;
         for (hipStream_t s : {p.compute, p.edge, p.copy})
             if (s) (void)hipStreamSynchronize(s);
+        if (p.comm) (void)Rccl::get().destroy(static_cast<ncclComm_t>(p.comm));
         for (auto b : p.buf)
             if (b) (void)hipFree(b);
         if (p.acc) (void)hipFree(p.acc);
@@ -269,13 +363,9 @@ int MultiBoard::reduce(bool hash, uint64_t* out) {
 //   compute[i]: wait ev_edge[i]
 // A copy into part j's ghost rows is ordered after j's previous pass has read them: the copying part's
 // previous pass waited for j's copies, which waited for j's pass before that.
-int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
-    for (size_t i = 0; i < parts_.size(); i++) {
-        Part& p = parts_[i];
-        GOL_MHIP(hipSetDevice(p.device));
-        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].t0, p.compute));
-        GOL_MHIP(hipEventRecord(p.ev_start, p.compute));
-    }
+// Peer copies: each part pushes its edge rows into its neighbours' ghost rows on its copy stream (after its own
+// previous pass); a part's edge bands then wait for its NEIGHBOURS' copy streams.
+int MultiBoard::exchange_peer(int k) {
     const size_t row_bytes = (size_t)W_ / 8;  // pitch == width / 32 words
     for (Part& p : parts_) {
         GOL_MHIP(hipSetDevice(p.device));
@@ -294,6 +384,49 @@ int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
         }
         GOL_MHIP(hipEventRecord(p.ev_copied, p.copy));
     }
+    return GOL_OK;
+}
+
+// RCCL: every part's sends and receives of the pass in ONE group (one thread drives every communicator), issued
+// in exchange_plan's order on each part's copy stream after that part's previous pass; a part's edge bands then
+// wait for its OWN copy stream, where its receives complete.
+int MultiBoard::exchange_rccl(int k) {
+    const Rccl& nc = Rccl::get();
+    const std::vector<gol_xfer> plan = exchange_plan(H_, boundary_, (int)parts_.size(), max_k_, k);
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipStreamWaitEvent(p.copy, p.ev_start, 0));
+    }
+    ncclResult_t r = nc.group_start();
+    if (r != ncclSuccess) return api_fail(GOL_ERR_HIP, "ncclGroupStart: " + nc.why(r));
+    for (const gol_xfer& x : plan) {
+        Part& p = parts_[(size_t)x.part];
+        uint32_t* rows = p.buf[cur_] + x.row * p.s.pitch;
+        const size_t bytes = (size_t)(x.nrows * p.s.pitch) * 4;
+        r = x.op == 0 ? nc.send(rows, bytes, ncclUint8, x.peer, static_cast<ncclComm_t>(p.comm), p.copy)
+                      : nc.recv(rows, bytes, ncclUint8, x.peer, static_cast<ncclComm_t>(p.comm), p.copy);
+        if (r != ncclSuccess) {
+            (void)nc.group_end();
+            return api_fail(GOL_ERR_HIP, std::string(x.op == 0 ? "ncclSend: " : "ncclRecv: ") + nc.why(r));
+        }
+    }
+    r = nc.group_end();
+    if (r != ncclSuccess) return api_fail(GOL_ERR_HIP, "ncclGroupEnd: " + nc.why(r));
+    for (Part& p : parts_) {
+        GOL_MHIP(hipSetDevice(p.device));
+        GOL_MHIP(hipEventRecord(p.ev_copied, p.copy));
+    }
+    return GOL_OK;
+}
+
+int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
+    for (size_t i = 0; i < parts_.size(); i++) {
+        Part& p = parts_[i];
+        GOL_MHIP(hipSetDevice(p.device));
+        if (timers) GOL_MHIP(hipEventRecord((*timers)[i].t0, p.compute));
+        GOL_MHIP(hipEventRecord(p.ev_start, p.compute));
+    }
+    GOL_MRC(rccl_ ? exchange_rccl(k) : exchange_peer(k));
     for (size_t i = 0; i < parts_.size(); i++) {
         Part& p = parts_[i];
         GOL_MHIP(hipSetDevice(p.device));
@@ -312,8 +445,12 @@ int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
         }
         if (timers) GOL_MHIP(hipEventRecord((*timers)[i].interior, p.compute));
         GOL_MHIP(hipStreamWaitEvent(p.edge, p.ev_start, 0));
-        for (int q : {p.up, p.down})
-            if (q >= 0) GOL_MHIP(hipStreamWaitEvent(p.edge, parts_[(size_t)q].ev_copied, 0));
+        if (rccl_) {
+            GOL_MHIP(hipStreamWaitEvent(p.edge, p.ev_copied, 0));  // my receives landed
+        } else {
+            for (int q : {p.up, p.down})
+                if (q >= 0) GOL_MHIP(hipStreamWaitEvent(p.edge, parts_[(size_t)q].ev_copied, 0));
+        }
         if (timers) GOL_MHIP(hipEventRecord((*timers)[i].go, p.edge));
         GOL_MRC(gol_strip_step(&p.s, src, dst, k, 0, lo, p.edge));
         GOL_MRC(gol_strip_step(&p.s, src, dst, k, hi, rows, p.edge));

@@ -1,6 +1,12 @@
 // gol_multi.h -- one board handle over several GPUs of one process (gol_create with num_gpus > 1,
 // gol_create_multi).  Not installed; gol_capi.cpp dispatches the public entry points here.
 //
+// Halo transport: RCCL (ncclSend / ncclRecv inside ncclGroupStart / End, one communicator per part from
+// ncclCommInitAll over the parts' devices: xGMI between MI355X GPUs) when every part has its own device; peer
+// copies (hipMemcpyPeerAsync) when a device repeats -- RCCL refuses two ranks on one GPU, and that is the one-GPU
+// rehearsal of the protocol.  Both follow the same plan (exchange_plan), checked on the CPU by
+// tests/test_exchange_order.py.
+//
 // The reference's host is ONE process (the F# driver, GameOfLifeDriver.fs:13-41), so a drop-in that
 // spreads the board over the GPUs of a node must do it behind one handle.  Layout: row strips, part r
 // owning global rows [y0_r, y0_r + rows_r) on devices[r], in the gol_strip geometry of include/gol/gol.h
@@ -21,6 +27,13 @@ namespace gol {
 
 int api_fail(int code, const std::string& msg);  // sets gol_last_error (gol_capi.cpp)
 
+// The halo messages of one pass, in the order each part issues them (include/gol/gol.h gol_xfer): part r sends its
+// top k owned rows to `up` and its bottom k rows to `down`, then receives the down neighbour's top rows below its
+// owned rows and the up neighbour's bottom rows above them.  RCCL pairs a sender's sends to one peer with that
+// peer's receives from it in issue order (tags are ignored), which this order satisfies even when up == down (two
+// parts on a torus).  Rows are buffer rows (0 = the first of `ghost` halo rows above the owned rows).
+std::vector<gol_xfer> exchange_plan(int64_t height, int boundary, int nparts, int64_t ghost, int k);
+
 class MultiBoard {
    public:
     struct Part {
@@ -31,6 +44,7 @@ class MultiBoard {
         hipStream_t compute = nullptr, edge = nullptr, copy = nullptr;
         hipEvent_t ev_start = nullptr, ev_copied = nullptr, ev_edge = nullptr;
         int up = -1, down = -1;  // neighbour parts (-1: bounded board edge)
+        void* comm = nullptr;    // ncclComm_t of this part (RCCL transport)
     };
 
     // creates the parts; returns GOL_OK or a GOL_ERR_* code (the object is then unusable)
@@ -58,13 +72,20 @@ class MultiBoard {
     int cur() const { return cur_; }
     hipStream_t stream0() const { return parts_.empty() ? nullptr : parts_[0].compute; }
     int max_k() const { return max_k_; }
+    int transport() const { return rccl_ ? GOL_TRANSPORT_RCCL : GOL_TRANSPORT_PEER; }
+    const std::string& transport_note() const { return transport_note_; }
 
    private:
     struct PassTimer {  // timing events of one part, recorded only by timed_pass
         hipEvent_t t0 = nullptr, interior = nullptr, go = nullptr, edge = nullptr;
     };
     int pass(int k, std::vector<PassTimer>* timers = nullptr);
+    int exchange_peer(int k);
+    int exchange_rccl(int k);
+    int init_rccl();
     std::vector<Part> parts_;
+    bool rccl_ = false;
+    std::string transport_note_;
     int64_t W_ = 0, H_ = 0;
     int boundary_ = GOL_TORUS, ilv_ = 1, tblock_ = 1, max_k_ = 1;
     int cur_ = 0;

@@ -145,15 +145,12 @@ int segments(int64_t cols, int64_t H, int nt) {
     return (int)(s < H ? s : H);
 }
 
-// Workgroup size: 1024 threads unless GOL_RESIDENT_THREADS=256 (A/B of the barrier cost on tiny boards).
-int resident_threads() {
-    const char* e = std::getenv("GOL_RESIDENT_THREADS");
-    return e && std::atoi(e) == 256 ? 256 : 1024;
-}
-
+// Workgroup size: 1024 threads unless the board's "resident_threads" option is 256 (A/B of the barrier cost on
+// tiny boards: 256 was slower everywhere, profiles/r1/resident_threads_ab.log).
 template <bool BOUNDED>
-void launch_packed(const uint32_t* src, uint32_t* dst, int wpr, int H, int64_t pitch, int gens, hipStream_t s) {
-    if (resident_threads() == 256)
+void launch_packed(const uint32_t* src, uint32_t* dst, int wpr, int H, int64_t pitch, int gens, hipStream_t s,
+                   int threads) {
+    if (threads == 256)
         hipLaunchKernelGGL((gol_resident_packed<BOUNDED, 256>), dim3(1), dim3(256), 0, s, src, dst, wpr, H, pitch,
                            gens, segments(wpr, H, 256));
     else
@@ -162,8 +159,8 @@ void launch_packed(const uint32_t* src, uint32_t* dst, int wpr, int H, int64_t p
 }
 
 template <bool BOUNDED>
-void launch_bytes(const uint8_t* src, uint8_t* dst, int W, int H, int gens, hipStream_t s) {
-    if (resident_threads() == 256)
+void launch_bytes(const uint8_t* src, uint8_t* dst, int W, int H, int gens, hipStream_t s, int threads) {
+    if (threads == 256)
         hipLaunchKernelGGL((gol_resident_bytes<BOUNDED, 256>), dim3(1), dim3(256), 0, s, src, dst, W, H, gens,
                            segments(W, H, 256));
     else
@@ -180,22 +177,22 @@ bool resident_packed_fits(int64_t W, int64_t H) {
 bool resident_bytes_fits(int64_t W, int64_t H) { return W >= 1 && H >= 1 && 2 * W * H <= kLdsBytes; }
 
 hipError_t launch_resident_packed(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch,
-                                  int64_t gens, bool bounded, hipStream_t s) {
+                                  int64_t gens, bool bounded, hipStream_t s, int threads) {
     if (!resident_packed_fits(W, H) || pitch < W / 32 || gens < 1 || gens > INT32_MAX) return hipErrorInvalidValue;
     if (bounded)
-        launch_packed<true>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s);
+        launch_packed<true>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s, threads);
     else
-        launch_packed<false>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s);
+        launch_packed<false>(src, dst, (int)(W / 32), (int)H, pitch, (int)gens, s, threads);
     return hipGetLastError();
 }
 
 hipError_t launch_resident_bytes(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, int64_t gens, bool bounded,
-                                 hipStream_t s) {
+                                 hipStream_t s, int threads) {
     if (!resident_bytes_fits(W, H) || gens < 1 || gens > INT32_MAX) return hipErrorInvalidValue;
     if (bounded)
-        launch_bytes<true>(src, dst, (int)W, (int)H, (int)gens, s);
+        launch_bytes<true>(src, dst, (int)W, (int)H, (int)gens, s, threads);
     else
-        launch_bytes<false>(src, dst, (int)W, (int)H, (int)gens, s);
+        launch_bytes<false>(src, dst, (int)W, (int)H, (int)gens, s, threads);
     return hipGetLastError();
 }
 

@@ -669,14 +669,9 @@ int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap) {
 // share a SIMD.  VALU issue favours the older wave (MI355X_MICROARCH.md "Two waves per SIMD"), so with
 // equal segments it finishes early and leaves the younger alone at the single-wave issue rate
 // (tools/tail.py: 65536^2, K = 16 -- waves 0-3 of every workgroup busy 489 us, waves 4-7 747 us).
-// GOL_SPLIT=<fraction> overrides (experiments); 0 disables.
+// A board's "split" option (gol_set_option) overrides it for experiments.
 int stream_pair_split(int k, int ilv, bool bounded) {
-    static const int env = [] {
-        const char* e = std::getenv("GOL_SPLIT");
-        return e ? (int)(std::atof(e) * 65536.0) : -1;
-    }();
     if (kWavesPerBlock < 8) return 0;
-    if (env >= 0) return env;
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
     // (12, 2) runs 12-wave workgroups at 3 waves/SIMD: three-way groups (profiles/r1/w12_sweep*.log)
@@ -719,13 +714,10 @@ static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool 
 // Work decomposition: nstrips column strips x nsegs row segments, one wave each (or one SIMD group of
 // waves per segment with the pair split).  The segment count makes the grid ONE balanced round of
 // resident waves (a partial second round would leave a tail of lone waves), with segments no shorter than
-// 2K rows (pipeline fill cost).  GOL_SEG_ROWS overrides the segment length (experiments).
+// 2K rows (pipeline fill cost).  a.split_opt / a.seg_opt (a board's "split" / "seg_rows" options) override
+// the split and the segment length for experiments.
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
-    static const int64_t env_seg = [] {
-        const char* e = std::getenv("GOL_SEG_ROWS");
-        return e ? std::atoll(e) : 0LL;
-    }();
-    a.split = stream_pair_split(k, a.ilv, bounded);
+    a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded));
     a.nstrips = stream_strips(a.words, a.ilv, k, bounded);
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
@@ -737,7 +729,7 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     // segment: splitting a handful of rows only multiplies the pipeline fill
     const int wpb = stream_wpb(a.words, k, a.ilv, bounded, wrap);
     if (a.split && rows < (int64_t)(wpb / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
-    int64_t seg = env_seg;
+    int64_t seg = a.seg_opt;
     if (seg <= 0) {
         const int group = a.split ? wpb / 4 : 1;  // waves per segment
         int64_t units = resident_units(a.words, k, a.ilv, bounded, wrap);

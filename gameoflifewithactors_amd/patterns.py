@@ -15,6 +15,29 @@ import struct
 
 import numpy as np
 
+# BASELINE config 5's seeds: the Gosper glider gun (36 cells, period 30) and the R-pentomino
+GOSPER_GUN = ("24bo$22bobo$12b2o6b2o12b2o$11bo3bo4b2o12b2o$2o8bo5bo3b2o$2o8bo3bob2o4bobo$10bo5bo7bo$11bo3bo$"
+              "12b2o!")
+R_PENTOMINO = "b2o$2o$bo!"
+NAMED = {"gosper-gun": GOSPER_GUN, "r-pentomino": R_PENTOMINO}
+
+
+def parse_placements(spec: str) -> list:
+    """'NAME_OR_FILE[@x,y]+...' -> [(rle text, x, y)]: a named pattern (gosper-gun, r-pentomino) or an RLE file,
+    its top-left at (x, y) (default 0, 0)."""
+    out = []
+    for part in spec.split("+"):
+        what, _, at = part.partition("@")
+        x, y = (int(v) for v in at.split(",")) if at else (0, 0)
+        if what in NAMED:
+            text = NAMED[what]
+        else:
+            with open(what) as f:
+                text = f.read()
+        out.append((text, x, y))
+    return out
+
+
 MAGIC = b"GOLSNAP1"
 _HEADER = struct.Struct("<8sqqiiqQ")  # magic, width, height, boundary, reserved, generation, hash
 

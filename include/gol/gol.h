@@ -71,6 +71,11 @@ int gol_create_multi(int64_t width, int64_t height, int boundary, const int* dev
  * first global row, owned rows and halo depth (ghost rows per side; 0 for a single board). */
 int gol_num_parts(gol_board* b, int* n);
 int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* rows, int64_t* ghost);
+/* How a multi-part board moves its halo rows: RCCL send/recv (ncclCommInitAll over the parts' devices, xGMI) when
+ * every part has its own device, else peer copies (a device repeats: RCCL refuses two ranks on one GPU); a
+ * single board has none.  note (may be NULL, >= 256 bytes): why, e.g. the RCCL error that made it fall back. */
+enum { GOL_TRANSPORT_NONE = 0, GOL_TRANSPORT_PEER = 1, GOL_TRANSPORT_RCCL = 2 };
+int gol_transport(gol_board* b, int* transport, char* note, int64_t note_len);
 int gol_destroy(gol_board* b);
 
 /* Board I/O: cells[x + y*width], len == width*height.  Replaces createCell's `alive` argument
@@ -97,10 +102,10 @@ int gol_place_rle(gol_board* b, const char* rle, int64_t x, int64_t y);
 int gol_clear(gol_board* b);
 
 /* Advance `generations` synchronous B3/S23 generations (GameOfLifeLogic.fs:47-66 under the Reset->State
- * phase barrier).  Asynchronous with respect to the host; any readback synchronises.  Small and mid-size
- * boards run the whole call as one launch (single-wave, cooperative or LDS-resident pass: DESIGN.md 4.3;
- * env GOL_WAVE_RESIDENT, GOL_COOP and GOL_RESIDENT_MAX_CELLS override the cut-overs); results are identical
- * either way. */
+ * phase barrier).  Asynchronous with respect to the host; any readback synchronises (and reports a failed
+ * cooperative pass: the board is then invalid until overwritten).  Small and mid-size boards run the whole call
+ * as one launch (single-wave, cooperative or LDS-resident pass: DESIGN.md 4.3-4.5; gol_set_option moves the
+ * cut-overs); results are identical either way. */
 int gol_step(gol_board* b, int64_t generations);
 int gol_generation(gol_board* b, int64_t* out);
 int gol_synchronize(gol_board* b);
@@ -130,9 +135,27 @@ int gol_stream(gol_board* b, void** stream);
 /* Profiling: advance the board by ONE pass of its temporal depth with HIP timing events and report, per
  * row strip (n = gol_num_parts), the microseconds from the pass start to the end of the interior launch
  * (interior_us), to the release of the edge-band stream once the neighbours' halo rows have landed
- * (wait_us: the edge-band wait) and to the end of the edge bands (edge_us).  A single board reports its
- * one launch in interior_us and edge_us and 0 in wait_us.  Counts toward gol_generation. */
+ * (wait_us: the edge-band wait) and to the end of the edge bands (edge_us).  A single board times one
+ * streaming pass and reports it in interior_us and edge_us and 0 in wait_us; a single board whose gol_step
+ * runs another pass (single-wave, cooperative, LDS-resident) returns GOL_ERR_UNSUPPORTED.  Counts toward
+ * gol_generation. */
 int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, double* edge_us);
+
+/* Per-board path and tuning options (the library reads no environment variable).  Names, defaults first:
+ *   "coop" 1 | 0                 cooperative register-band pass for mid-size boards
+ *   "coop_k" 0 | 1..64           generations per band hand-off (0: min(tblock_k, 8))
+ *   "coop_max_cells" 2^26        largest board that pass takes
+ *   "resident_max_cells" -1 | n  LDS-resident pass cut-over (-1: 2^17 packed cells, off for byte boards; 0: off)
+ *   "wave_resident" 1 | 0        single-wave pass for boards up to 128 x 256
+ *   "split" 0 | n | -1           streaming pass: the oldest wave's share of a SIMD group segment in 1/65536
+ *                                (0: the measured default, -1: no split)
+ *   "seg_rows" 0 | n             streaming pass: rows per wave segment (0: planned)
+ *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments
+ *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
+ *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)
+ * Unknown names and out-of-range values return GOL_ERR_INVALID.  Results are bit-identical for every setting. */
+int gol_set_option(gol_board* b, const char* name, int64_t value);
+int gol_get_option(gol_board* b, const char* name, int64_t* value);
 
 const char* gol_last_error(void);
 const char* gol_version(void);
@@ -177,6 +200,16 @@ int gol_strip_population(const gol_strip* s, const uint32_t* buf, uint64_t* dev_
 int gol_strip_hash_partial(const gol_strip* s, const uint32_t* buf, uint64_t* dev_acc, void* stream);
 /* Combine the (wrapping) sum of every strip's partial into the canonical board hash. */
 uint64_t gol_hash_finalize(uint64_t partial_sum, int64_t width, int64_t height);
+/* The halo messages of one pass of a multi-part board (one process, gol_create num_gpus > 1), in the order each
+ * part issues them -- the plan both transports execute: op 0 = send, 1 = recv; rows are buffer rows of the part
+ * (0 = the first of `ghost` halo rows).  Host-only (no device needed): tests check that every receive gets the
+ * rows the topology gives it under RCCL's in-order pairing. */
+typedef struct gol_xfer {
+    int32_t part, op, peer, pad;
+    int64_t row, nrows;
+} gol_xfer;
+int gol_exchange_plan(int64_t height, int boundary, int nparts, int64_t ghost, int k, gol_xfer* ops, int64_t max_ops,
+                      int64_t* n_ops);
 /* Number of wavefront column strips / rows per segment the step kernel uses (for roofline accounting). */
 int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves,
                    int64_t* seg_rows);

@@ -30,19 +30,3 @@ def oracle():
     import gol_oracle
 
     return gol_oracle
-
-
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first():
-    """Initialise torch's HIP runtime before any test loads libgol_hip.so through ctypes.  torch ships its own
-    HIP runtime; when the library's (/opt/rocm) initialises first in a process, torch's later lazy init can
-    fail with "No HIP GPUs are available" (seen on the GPU box when a torch-using test ran after C-ABI-only
-    tests).  bench.py and strips.py always initialise torch first.  No-op on a host without a GPU."""
-    try:
-        import torch
-
-        if torch.cuda.is_available():
-            torch.cuda.init()
-    except Exception:
-        pass
-    yield

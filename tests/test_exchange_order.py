@@ -106,3 +106,56 @@ def test_world2_torus_order_is_what_makes_nccl_pair_it(monkeypatch):
     _deliver(ranks, swapped, "nccl")
     with pytest.raises(AssertionError):
         _check_ghosts(ranks, 64, TORUS, 4)
+
+
+# ---------------------------------------------------------------- the one-process handle (csrc/gol_multi.cpp)
+def _deliver_plan(plan, nparts, height, ghost, boundary, k):
+    """Execute gol_exchange_plan's messages under RCCL pairing (per (sender, receiver) in issue order) on buffers
+    whose every row holds its global row index (-1 = not written), and check every part's ghost rows."""
+    y0 = [height * r // nparts for r in range(nparts)]
+    rows = [height * (r + 1) // nparts - y0[r] for r in range(nparts)]
+    bufs = []
+    for r in range(nparts):
+        b = [-1] * (rows[r] + 2 * ghost)
+        for i in range(rows[r]):
+            b[ghost + i] = y0[r] + i
+        bufs.append(b)
+    sends, recvs = defaultdict(list), defaultdict(list)
+    for part, op, peer, row, n in plan:
+        assert n == k
+        (sends[(part, peer)] if op == "send" else recvs[(peer, part)]).append((part, row))
+    assert sorted(sends) == sorted(recvs), "a send has no matching receive: RCCL would hang"
+    for key in sends:
+        assert len(sends[key]) == len(recvs[key]), key
+        for (sp, srow), (rp, rrow) in zip(sends[key], recvs[key]):
+            bufs[rp][rrow:rrow + k] = bufs[sp][srow:srow + k]
+    for r in range(nparts):
+        for i in range(k):
+            for row, gy in ((ghost - k + i, y0[r] - k + i), (ghost + rows[r] + i, y0[r] + rows[r] + i)):
+                want = gy % height if boundary == TORUS else (gy if 0 <= gy < height else -1)
+                assert bufs[r][row] == want, (r, row, gy)
+
+
+@pytest.mark.parametrize("nparts,height,boundary,ghost,k", [
+    (2, 64, TORUS, 12, 12), (2, 64, TORUS, 12, 8), (2, 64, BOUNDED, 16, 12), (3, 91, TORUS, 8, 8),
+    (3, 91, BOUNDED, 8, 4), (4, 100, TORUS, 16, 16), (5, 333, TORUS, 12, 1), (8, 8 * 32, TORUS, 12, 12),
+    (8, 8 * 32 + 5, BOUNDED, 12, 12), (8, 65536 * 8, TORUS, 12, 12),
+])
+def test_handle_exchange_plan_pairs_under_rccl(nparts, height, boundary, ghost, k):
+    """The one-process multi-GPU handle (gol_create num_gpus > 1) moves its halo rows with RCCL send/recv when every
+    part has its own GPU (csrc/gol_multi.cpp exchange_rccl) and with peer copies otherwise; both execute
+    gol_exchange_plan.  Under RCCL pairing (tags ignored, per-peer issue order) every receive must get the rows the
+    topology gives it: torus wrap (GameOfLifeDriver.fs:21-25), nothing beyond a bounded board (Script.fsx:6-13)."""
+    from gameoflifewithactors_amd import _lib
+
+    plan = _lib.exchange_plan(height, boundary, nparts, ghost, k)
+    _deliver_plan(plan, nparts, height, ghost, boundary, k)
+
+
+def test_handle_exchange_plan_rejects_bad_geometry():
+    from gameoflifewithactors_amd import _lib
+
+    with pytest.raises(ValueError):
+        _lib.exchange_plan(64, TORUS, 2, 4, 8)  # ghost < k
+    with pytest.raises(ValueError):
+        _lib.exchange_plan(20, TORUS, 4, 8, 8)  # parts of 5 rows are thinner than k

@@ -5,8 +5,8 @@ call as one persistent launch: one workgroup per CU holds a band of rows in regi
 rows through LDS every generation and hands its K edge rows to its two neighbour bands every K generations.
 Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus GameOfLifeDriver.fs:21-25; bounded
 Script.fsx:6-13), the BASELINE config-2 golden checkpoints (4096^2, .NET Random seed 42, 10k generations), and
-the streaming pass on the same board (GOL_COOP=0).  Uneven bands (heights that do not divide over the CUs),
-bands shorter than two blocks, several block depths (GOL_COOP_K), both word layouts (consecutive words of an
+the streaming pass on the same board (board option "coop" 0).  Uneven bands (heights that do not divide over the CUs),
+bands shorter than two blocks, several block depths ("coop_k"), both word layouts (consecutive words of an
 ilv-1 board, interleaved blocks of an ilv-2 / ilv-4 board), ragged byte boards (widths not a multiple of 32,
 through whole-word scratch rows) and split calls are covered.
 """
@@ -34,32 +34,14 @@ def _rand(h, w, seed, p=0.45):
     return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
 
 
-class _Env:
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update({k: str(v) for k, v in self.kv.items()})
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 def _run(gol, b0, boundary, steps, coop, k=None, ilv=0):
     h, w = b0.shape
-    env = {"GOL_COOP": "1" if coop else "0"}
+    opts = {"coop": int(coop)}
     if k:
-        env["GOL_COOP_K"] = str(k)
-    with _Env(**env), gol.Board(w, h, boundary, ilv=ilv) as b:
-        if coop and not ilv and w in (4096, 8192):
-            assert b.info()["ilv"] == w // 2048  # the pass's interleaved layout
-        elif not ilv:
-            assert b.info()["ilv"] == 1
+        opts["coop_k"] = k
+    with gol.Board(w, h, boundary, ilv=ilv, options=opts) as b:
+        if not ilv:  # single boards of the widths the pass holds interleaved get its layout, on either path
+            assert b.info()["ilv"] == (w // 2048 if w in (4096, 8192) else 1)
         b.set_cells(b0)
         for g in steps:
             b.step(g)
@@ -98,7 +80,7 @@ def test_coop_config2_golden_checkpoints(gol):
     population every 100 generations) to generation 10,000, on the cooperative pass."""
     with open(os.path.join(HERE, "golden", "golden_long.json")) as f:
         case = json.load(f)["c2_4096_torus_dotnet42"]
-    with _Env(GOL_COOP="1"), gol.Board(case["width"], case["height"], case["boundary"]) as b:
+    with gol.Board(case["width"], case["height"], case["boundary"], options={"coop": 1}) as b:
         b.seed_dotnet(case["seed"], gol.INIT_DOTNET_MOD2)
         done = 0
         for gen, h, pop in case["checkpoints"]:
@@ -109,20 +91,46 @@ def test_coop_config2_golden_checkpoints(gol):
 
 def test_coop_epoch_wrap(gol, oracle):
     """The hand-off granules carry a 16-bit launch epoch; at the wrap the host clears them. Launches just before,
-    at and after the wrap (GOL_COOP_EPOCH sets the epoch of the last launch) must stay exact."""
+    at and after the wrap (the "coop_epoch" option sets the epoch of the last launch) must stay exact."""
     b0 = _rand(1024, 1024, 77)
-    with _Env(GOL_COOP="1"), gol.Board(1024, 1024, 0) as b:
+    with gol.Board(1024, 1024, 0, options={"coop": 1}) as b:
         b.set_cells(b0)
         b.step(9)  # first launch: allocates and clears the exchange buffer
         done = 9
         for epoch in (0xfffd, 0xfffe, 0xffff):
-            with _Env(GOL_COOP_EPOCH=str(epoch)):
-                b.step(17)  # this launch runs at epoch + 1 (the last one wraps to 1 and clears)
+            b.set_option("coop_epoch", epoch)
+            b.step(17)  # this launch runs at epoch + 1 (the last one wraps to 1 and clears)
             done += 17
         b.step(17)
         done += 17
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, done, 0))
 
+
+def test_coop_timeout_reported_on_every_readback(gol, oracle):
+    """A band hand-off wait that times out (forced here: a spin limit of one poll, while the neighbour band has not
+    published yet) leaves a wrong board.  Every readback and gol_synchronize must report it (GOL_ERR_HIP), the
+    launch must still end (no further waits once one has failed), and the board must be usable again once it is
+    overwritten."""
+    b0 = _rand(2048, 2048, 91)
+    with gol.Board(2048, 2048, 0, options={"coop": 1, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
+        b.set_cells(b0)
+        failed = False
+        for _ in range(20):  # the race is lost almost always at once; a few tries make it certain
+            b.step(200)
+            try:
+                b.synchronize()
+            except RuntimeError:
+                failed = True
+                break
+        assert failed, "a one-poll spin limit never timed out"
+        for call in (b.get_cells, b.hash, b.population, b.save_packed, lambda: b.get_region(0, 0, 8, 8),
+                     b.synchronize):
+            with pytest.raises(RuntimeError, match="hand-off timed out"):
+                call()
+        b.set_option("coop_spin_limit", 0)  # back to the default limit
+        b.set_cells(b0)  # overwritten: valid again
+        b.step(37)
+        np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 37, 0))
 
 
 @pytest.mark.parametrize("boundary", [0, 1])
@@ -133,12 +141,12 @@ def test_coop_ragged_widths(gol, oracle, w, h, boundary):
     the cooperative pass through whole-word scratch rows (calls of >= 16 generations), with the row end patched
     at bit level: torus wrap from cell W - 1 to cell 0 (GameOfLifeDriver.fs:21-25), dead beyond both ends when
     bounded (Script.fsx:6-13).  Rows of 1, 2 and 4 words per lane, padded rows (2049, 4097), split calls and a
-    remainder block, against the oracle and against the per-generation byte step (GOL_COOP=0)."""
+    remainder block, against the oracle and against the per-generation byte step ("coop" 0)."""
     b0 = _rand(h, w, w + 7 * h + boundary)
     steps = [16, 3, 21]  # 3 < 16: the byte step between two pass calls
     want = oracle.c_run(b0, sum(steps), boundary)
     for coop in (True, False):
-        with _Env(GOL_COOP="1" if coop else "0"), gol.Board(w, h, boundary) as b:
+        with gol.Board(w, h, boundary, options={"coop": int(coop)}) as b:
             assert not b.info()["packed"]
             b.set_cells(b0)
             for g in steps:
@@ -151,7 +159,7 @@ def test_coop_ragged_byte_values(gol, oracle):
     """Byte cells are alive when nonzero (any value); the ragged pass writes the board back as 0 / 1."""
     b0 = _rand(200, 1001, 5)
     vals = (b0 * np.random.default_rng(6).integers(1, 256, size=b0.shape)).astype(np.uint8)
-    with _Env(GOL_COOP="1"), gol.Board(1001, 200, 0) as b:
+    with gol.Board(1001, 200, 0, options={"coop": 1}) as b:
         b.set_cells(vals)
         b.step(24)
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 24, 0))

@@ -160,3 +160,12 @@ def test_calls_restore_the_callers_device(gol, oracle):
         assert x.device.index == 1
     finally:
         torch.cuda.set_device(0)
+
+
+def test_transport_on_one_gpu_is_peer_copies(gol):
+    """Strips that share a device move their halo rows by peer copies (RCCL needs one rank per GPU); a single
+    board has no exchange (gol_transport)."""
+    with gol.Board(1024, 256, 0, devices=[0, 0, 0]) as b:
+        assert b.transport().startswith("peer:"), b.transport()
+    with gol.Board(1024, 256, 0) as b:
+        assert b.transport().startswith("none:")

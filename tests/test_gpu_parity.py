@@ -307,41 +307,19 @@ def test_long_run_checkpoints(gol, oracle, name, tblock):
         assert b.generation == case["generations"]
 
 
-_SPLIT_SCRIPT = r"""
-import json, os, sys
-import numpy as np
-root = os.environ["GOL_TEST_ROOT"]
-sys.path[:0] = [root, os.path.join(root, "oracle")]
-import gameoflifewithactors_amd as g
-import gol_oracle as o
-out = []
-for boundary in (0, 1):
-    for w, h, k, ilv in ((4096, 1500, 12, 2), (4096, 700, 16, 2), (2048, 900, 32, 1), (4096, 600, 8, 4)):
-        b0 = (np.random.default_rng(w + h + k + boundary).random((h, w)) < 0.4).astype(np.uint8)
-        gens = 2 * k + 5
-        with g.Board(w, h, boundary, tblock_k=k, ilv=ilv) as b:
-            b.set_cells(b0).step(gens)
-            ok = bool(np.array_equal(b.get_cells(), o.c_run(b0, gens, boundary)))
-        out.append([boundary, w, h, k, ilv, ok])
-print(json.dumps(out))
-"""
-
-
-@pytest.mark.parametrize("split", ["0.95", "0.3", "0.5"])
-def test_group_split_extremes_match_oracle(split):
+@pytest.mark.parametrize("split", [0.95, 0.3, 0.5])
+def test_group_split_extremes_match_oracle(gol, oracle, split):
     """Segments shared by the waves of a SIMD (age-ordered shares, plan_stream / group_cut) at extreme
-    split fractions -- an empty or near-empty share for some waves -- stay bit-exact (child process so
-    GOL_SPLIT takes effect)."""
-    import json
-    import subprocess
-    import sys
-
-    root = os.path.dirname(HERE)
-    env = dict(os.environ, GOL_SPLIT=split, GOL_TEST_ROOT=root)
-    r = subprocess.run([sys.executable, "-c", _SPLIT_SCRIPT], capture_output=True, text=True, timeout=150, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert all(ok for *_, ok in res), res
+    split fractions -- an empty or near-empty share for some waves -- stay bit-exact (board option "split")."""
+    for boundary in (0, 1):
+        for w, h, k, ilv in ((4096, 1500, 12, 2), (4096, 700, 16, 2), (2048, 900, 32, 1), (4096, 600, 8, 4)):
+            b0 = (np.random.default_rng(w + h + k + boundary).random((h, w)) < 0.4).astype(np.uint8)
+            gens = 2 * k + 5
+            opts = {"split": int(split * 65536), "coop": 0}
+            with gol.Board(w, h, boundary, tblock_k=k, ilv=ilv, options=opts) as b:
+                b.set_cells(b0).step(gens)
+                np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, gens, boundary),
+                                              err_msg=f"{boundary} {w}x{h} k={k} ilv={ilv}")
 
 
 def test_concurrent_calls_on_one_handle_serialise(gol):
@@ -389,19 +367,18 @@ def test_native_host_mirror_driver():
 # ---------------------------------------------------------------- bounded boards: edge-fill strips
 @pytest.mark.parametrize("ilv", [1, 2])
 @pytest.mark.parametrize("nblocks", [64, 65, 124, 125, 126, 127, 189, 1024])
-def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks, monkeypatch):
+def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks):
     """Bounded boards at least a strip (64 blocks) wide place their first strip at the board's left edge and
     the last at its right edge (the dead cells beyond the edges arrive as the DPP moves' zero fill), and run
     only the trips that produce rows off the board masked (Script.fsx:6-13), in the variant without column
     masks (12-wave workgroups at K = 12).  Every strip-count boundary (nblocks around multiples of 62), the
     top/bottom trips of the first/last segments, a deep block and a remainder pass, against the oracle.  The
     cooperative pass is switched off so the streaming kernel runs every width."""
-    monkeypatch.setenv("GOL_COOP", "0")
     w = 32 * ilv * nblocks
     h = 300 if nblocks < 1024 else 64
     b0 = _rand(h, w, nblocks * 10 + ilv, p=0.4)
     for k in (16, 12, 8):
-        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv) as b:
+        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv, options={"coop": 0}) as b:
             assert b.info()["tblock_k"] == k
             b.set_cells(b0).step(2 * k + 5)
             np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 2 * k + 5, 1), err_msg=f"k={k}")
@@ -409,19 +386,18 @@ def test_bounded_edge_fill_strips_match_oracle(gol, oracle, ilv, nblocks, monkey
 
 @pytest.mark.parametrize("ilv", [1, 2])
 @pytest.mark.parametrize("nblocks", [1, 2, 31, 62, 63])
-def test_bounded_narrow_strips_match_oracle(gol, oracle, ilv, nblocks, monkeypatch):
+def test_bounded_narrow_strips_match_oracle(gol, oracle, ilv, nblocks):
     """Bounded boards narrower than one strip (< 64 blocks) take the NARROW streaming variant: lanes off the
     board, column masks at every level (Script.fsx:6-13).  The single-wave, cooperative and LDS-resident
     passes are switched off so the streaming kernel runs, at deep, mid and remainder depths."""
-    for key in ("GOL_COOP", "GOL_WAVE_RESIDENT", "GOL_RESIDENT_MAX_CELLS"):
-        monkeypatch.setenv(key, "0")
+    opts = {"coop": 0, "wave_resident": 0, "resident_max_cells": 0}
     w = 32 * ilv * nblocks
     h = 150
     if w < 3:
         pytest.skip("board narrower than 3 cells")
     b0 = _rand(h, w, nblocks * 7 + ilv, p=0.4)
     for k in (16, 12, 8):
-        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv) as b:
+        with gol.Board(w, h, gol.BOUNDED, tblock_k=k, ilv=ilv, options=opts) as b:
             if b.info()["tblock_k"] != k:
                 continue  # depth not supported at this layout
             b.set_cells(b0).step(2 * k + 5)

@@ -1,11 +1,11 @@
 """GPU parity of the LDS-resident small-board pass (csrc/gol_resident.hip).
 
-Boards up to 2^17 cells (packed ilv 1; with the cooperative pass off, GOL_COOP=0) or 2^14 cells (byte layout,
+Boards up to 2^17 cells (packed ilv 1; with the cooperative pass off, board option "coop" 0) or 2^14 cells (byte layout,
 widths not a multiple of 32) run a whole gol_step call as one launch with the board held in one workgroup's LDS; the kernel itself takes
-up to 2^19 / 2^16 cells, which these tests reach with GOL_RESIDENT_MAX_CELLS raised.  Bar: bit-exact against the oracle
+up to 2^19 / 2^16 cells, which these tests reach with the "resident_max_cells" option raised.  Bar: bit-exact against the oracle
 (GameOfLifeLogic.fs:56-63 rule, torus GameOfLifeDriver.fs:21-25, bounded Script.fsx:6-13) and against the
-streaming pass on the same board (GOL_RESIDENT_MAX_CELLS=0 forces the streaming pass; the C ABI reads the
-variable on every gol_step).
+streaming pass on the same board ("resident_max_cells" 0 forces the streaming pass).  The single-wave pass
+("wave_resident") is off in these runs so the shapes it would take exercise the pass they name.
 """
 import os
 
@@ -29,25 +29,16 @@ def _rand(h, w, seed, p=0.5):
 
 
 def _run(gol, b0, boundary, steps, resident):
-    # the cooperative pass (taken first for packed boards by default) is off here: LDS-resident vs streaming
+    # the single-wave and cooperative passes (taken first by default) are off here: LDS-resident vs streaming
+    # (resident_max_cells 0 forces the streaming pass, or the byte step on a ragged board)
     h, w = b0.shape
-    keys = ("GOL_RESIDENT_MAX_CELLS", "GOL_COOP")
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ["GOL_RESIDENT_MAX_CELLS"] = str(1 << 20) if resident else "0"
-    os.environ["GOL_COOP"] = "0"
-    try:
-        with gol.Board(w, h, boundary) as b:
-            b.set_cells(b0)
-            for g in steps:
-                b.step(g)
-            assert b.generation == sum(steps)
-            return b.get_cells()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    opts = {"resident_max_cells": (1 << 20) if resident else 0, "coop": 0, "wave_resident": 0}
+    with gol.Board(w, h, boundary, options=opts) as b:
+        b.set_cells(b0)
+        for g in steps:
+            b.step(g)
+        assert b.generation == sum(steps)
+        return b.get_cells()
 
 
 # (w, h): packed boards (w % 32 == 0) from one word per row to the 2^19-cell capacity, byte boards
@@ -85,20 +76,12 @@ def test_resident_byte_input_values_normalised(gol, oracle):
 # ---------------------------------------------------------------- single-wave register-resident pass
 def _run_wave(gol, b0, boundary, steps, wave):
     h, w = b0.shape
-    old = os.environ.get("GOL_WAVE_RESIDENT")
-    os.environ["GOL_WAVE_RESIDENT"] = "1" if wave else "0"
-    try:
-        with gol.Board(w, h, boundary) as b:
-            b.set_cells(b0)
-            for g in steps:
-                b.step(g)
-            assert b.generation == sum(steps)
-            return b.get_cells()
-    finally:
-        if old is None:
-            os.environ.pop("GOL_WAVE_RESIDENT", None)
-        else:
-            os.environ["GOL_WAVE_RESIDENT"] = old
+    with gol.Board(w, h, boundary, options={"wave_resident": int(wave)}) as b:
+        b.set_cells(b0)
+        for g in steps:
+            b.step(g)
+        assert b.generation == sum(steps)
+        return b.get_cells()
 
 
 # ragged (byte boards) and packed widths up to 128, heights up to 256 with 1-4 rows per lane; the

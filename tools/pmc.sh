@@ -7,8 +7,7 @@ tag=$1; k=$2; ilv=$3; groups=${4:-"1 2 3 4 5"}
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 out=gpurun_out/pmc_$tag
 mkdir -p $out
-export GOL_ILV=$ilv
-cmd="python3 tools/sweep.py --ks $k --passes 4 --boundary ${PMC_BOUNDARY:-0}"
+cmd="python3 tools/sweep.py --ilv $ilv --ks $k --passes 4 --boundary ${PMC_BOUNDARY:-0}"
 G[1]="FETCH_SIZE"
 G[2]="WRITE_SIZE"
 G[3]="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"

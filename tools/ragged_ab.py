@@ -1,5 +1,5 @@
 """Ragged byte boards (width not a multiple of 32, beyond the single-wave pass): the cooperative pass through
-whole-word scratch rows (GOL_COOP=1) against the per-generation byte step (GOL_COOP=0), interleaved, host wall
+whole-word scratch rows (option coop=1) against the per-generation byte step (coop=0), interleaved, host wall
 time around one gol_step call + gol_synchronize.  One JSON line per (board, pass, round)."""
 import json
 import os
@@ -13,8 +13,7 @@ BOARDS = [(255, 257, 2000), (1001, 1001, 1000), (2049, 2049, 1000), (4095, 4095,
 for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 2):
     for (w, h, gens) in BOARDS:
         for mode in ("1", "0"):
-            os.environ["GOL_COOP"] = mode
-            with Board(w, h, 0) as b:
+            with Board(w, h, 0, options={"coop": int(mode)}) as b:
                 b.seed_dotnet(42)
                 b.step(20)
                 b.synchronize()

@@ -1,6 +1,6 @@
 """Wall time of gol_step on the reference-size boards (BASELINE configs 1, 2, 5 and small-board sweep).
-Run with GOL_RESIDENT_MAX_CELLS=0 (streaming pass), GOL_WAVE_RESIDENT=0 (no single-wave pass) or neither
-(the default cut-overs); every line records both variables."""
+Arguments: board options name=value (gol_set_option, e.g. resident_max_cells=0 wave_resident=0 coop=0; none: the
+default cut-overs); every line records them."""
 import json
 import os
 import sys
@@ -15,17 +15,15 @@ CASES = [(100, 100, 0, 100, 'dotnet'), (100, 100, 0, 10000, 'dotnet'), (100, 100
          (512, 256, 0, 10000, 'dotnet'), (512, 512, 0, 10000, 'dotnet'), (1024, 512, 0, 10000, 'dotnet'), (1024, 1024, 0, 10000, 'dotnet'),
          (2048, 2048, 0, 4000, 'dotnet'), (4096, 4096, 1, 1000, 'dotnet'), (8192, 4096, 0, 1000, 'dotnet'),
          (255, 257, 0, 10000, 'dotnet')]
-mode = os.environ.get("GOL_RESIDENT_MAX_CELLS", "default")
-wave = os.environ.get("GOL_WAVE_RESIDENT", "default")
-coop = os.environ.get("GOL_COOP", "default") + ":" + os.environ.get("GOL_COOP_K", "8")
+opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[1:]}
 for (w, h, bnd, gens, seed) in CASES:
-    with Board(w, h, bnd) as b:
+    with Board(w, h, bnd, options=opts) as b:
         if seed == 'dotnet':
             b.seed_dotnet(42)
         else:
             b.place_rle("b2o$2o$bo!", w // 2, h // 2)
         b.step(2); b.synchronize()
         t0 = time.perf_counter(); b.step(gens); b.synchronize(); dt = time.perf_counter() - t0
-        print(json.dumps({"resident_max_cells": mode, "wave_resident": wave, "coop": coop, "w": w, "h": h, "boundary": bnd, "gens": gens,
+        print(json.dumps({"options": opts, "w": w, "h": h, "boundary": bnd, "gens": gens,
                           "ms": round(dt * 1e3, 3), "us_per_gen": round(dt / gens * 1e6, 3),
                           "gcups": round(w * h * gens / dt / 1e9, 2), "k": b.info()["tblock_k"]}), flush=True)

@@ -19,6 +19,8 @@ def main():
     p.add_argument("--ks", default="1,2,4,8,16,24,32")
     p.add_argument("--passes", type=int, default=8)
     p.add_argument("--boundary", type=int, default=0)
+    p.add_argument("--ilv", type=int, default=0, help="packed layout (0 = the engine default for the width)")
+    p.add_argument("--split", type=float, default=None, help="board option 'split' (fraction; negative = off)")
     a = p.parse_args()
     import torch
 
@@ -27,11 +29,14 @@ def main():
     W = a.size
     H = a.height or a.size
     lib = _lib.load()
-    ilv = lib.gol_default_ilv(W)  # honours GOL_ILV
+    ilv = a.ilv or lib.gol_default_ilv(W)
+    opts = {"coop": 0}
+    if a.split is not None:
+        opts["split"] = int(a.split * 65536) if a.split >= 0 else -1
     for k in [int(x) for x in a.ks.split(",")]:
         if not lib.gol_supported_k(k, ilv):
             continue
-        with Board(W, H, a.boundary, tblock_k=k) as b:
+        with Board(W, H, a.boundary, tblock_k=k, ilv=ilv, options=opts) as b:
             b.seed_splitmix(0x5EED)
             s = torch.cuda.ExternalStream(b.stream)
             b.step(2 * k)
