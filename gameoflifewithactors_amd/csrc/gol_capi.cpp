@@ -187,6 +187,8 @@ int board_ilv(int64_t width, int64_t height, int nparts) {
 }
 
 int board_tblock(int ilv, int64_t cells, int boundary) {
+    // byte boards (ragged widths): the ragged streaming pass runs ilv 1 words, as small ilv-1 boards do
+    if (ilv == 0) return cells < kSmallBoardCells ? 8 : 16;
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
     // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log).
     // Ghost-row strips (multi-GPU) keep K = 12: over a whole 10k-generation job 114k vs 100k GCUPS for
@@ -211,6 +213,9 @@ struct BoardOptions {
     bool wave_resident = true;                // "wave_resident": single-wave pass for boards <= 128 x 256
     int32_t split = 0;                        // "split": streaming pair split, 1/65536 (0 = engine, < 0 = off)
     int64_t seg_rows = 0;                     // "seg_rows": streaming rows per wave segment (0 = planned)
+    int seam = 0;                             // "seam": torus seam strips (0 = where they apply, -1 = off)
+    bool ragged_stream = true;                // "ragged_stream": ragged boards beyond the cooperative pass stream
+                                              // packed words (0: the per-generation byte step)
     int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
@@ -259,6 +264,7 @@ struct gol_board {
         a.ilv = ilv;
         a.split_opt = opt.split;
         a.seg_opt = opt.seg_rows;
+        a.seam_opt = opt.seam;
         return a;
     }
 };
@@ -471,6 +477,36 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     return GOL_OK;
 }
 
+// Whole-word scratch rows for a ragged byte board (two buffers of `need` words).
+int ensure_rag(gol_board* b, int64_t need) {
+    if (need <= b->rag_words) return GOL_OK;
+    GOL_HIP(hipStreamSynchronize(b->stream));
+    for (uint32_t*& r : b->rag) {
+        if (r) GOL_HIP(hipFree(r));
+        r = nullptr;
+    }
+    b->rag_words = 0;
+    for (uint32_t*& r : b->rag) {
+        const hipError_t e = hipMalloc(&r, (size_t)need * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            r = nullptr;
+            return fail(GOL_ERR_OOM, std::string("hipMalloc ragged scratch: ") + hipGetErrorString(e));
+        }
+    }
+    b->rag_words = need;
+    return GOL_OK;
+}
+
+// Ragged byte boards the cooperative pass does not take (wider than 8192 cells or above 2^26 cells) run the
+// streaming pass on whole-word scratch rows -- ceil(W / 32) words, the last one partial, the row end closed at bit
+// level (gol_step.hip kRagged; bounded: the column-masked variant) -- packed once per gol_step call of at least this
+// many generations; shorter calls take the per-generation byte step.
+constexpr int64_t kStreamRaggedMinGens = 4;
+bool use_stream_ragged(const gol_board* b) {
+    if (b->packed || b->W % 32 == 0 || !b->opt.ragged_stream) return false;
+    return (b->W + 31) / 32 >= 64;  // rows of at least one wave strip (the strip geometry's assumption)
+}
+
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
     if (gens > 0 && use_wave_resident(b)) {
@@ -491,21 +527,34 @@ int step_impl(gol_board* b, int64_t gens) {
     int64_t rag_pitch = 0;
     if (gens >= kCoopRaggedMinGens && use_coop_ragged(b, &rag_pitch)) {
         // the ragged byte board as whole words in scratch rows, the pass, and back to bytes
-        const int64_t need = rag_pitch * b->H;
-        if (need > b->rag_words) {
-            GOL_HIP(hipStreamSynchronize(b->stream));
-            for (uint32_t*& r : b->rag) {
-                if (r) GOL_HIP(hipFree(r));
-                r = nullptr;
-            }
-            b->rag_words = 0;
-            for (uint32_t*& r : b->rag) GOL_HIP(hipMalloc(&r, (size_t)need * sizeof(uint32_t)));
-            b->rag_words = need;
-        }
+        if (int rc = ensure_rag(b, rag_pitch * b->H)) return rc;
         GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, rag_pitch, b->stream));
         int rc_cur = 0;
         if (int rc = coop_steps(b, rag_pitch * 32, rag_pitch, 1, b->W, b->rag, &rc_cur, gens)) return rc;
         GOL_HIP(gol::launch_unpack_ragged(b->rag[rc_cur], b->cells(b->cur ^ 1), b->W, b->H, rag_pitch, b->stream));
+        b->cur ^= 1;
+        return GOL_OK;
+    }
+    if (gens >= kStreamRaggedMinGens && use_stream_ragged(b)) {
+        // the ragged byte board as whole words in scratch rows, streaming passes, and back to bytes
+        const int64_t nw = (b->W + 31) / 32;
+        if (int rc = ensure_rag(b, nw * b->H)) return rc;
+        GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, nw, b->stream));
+        int rc_cur = 0;
+        while (gens > 0) {
+            const int k = gol::stream_largest_k(gens, b->tblock, 1);
+            gol::StreamArgs a = b->stream_args(0, b->H, k);
+            a.words = nw;
+            a.pitch = nw;
+            a.ilv = 1;
+            a.rag_bits = (int32_t)(b->W % 32);
+            GOL_HIP(gol::launch_stream_step(b->rag[rc_cur], b->rag[rc_cur ^ 1], a, k, b->boundary == GOL_BOUNDED,
+                                            b->boundary == GOL_TORUS, b->stream));
+            rc_cur ^= 1;
+            b->generation += k;
+            gens -= k;
+        }
+        GOL_HIP(gol::launch_unpack_ragged(b->rag[rc_cur], b->cells(b->cur ^ 1), b->W, b->H, nw, b->stream));
         b->cur ^= 1;
         return GOL_OK;
     }
@@ -1121,6 +1170,8 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (value >= 65536) return fail(GOL_ERR_INVALID, "split must be < 65536 (1/65536 units; 0 default, < 0 off)");
         o.split = (int32_t)(value < 0 ? -1 : value);
     } else if (n == "seg_rows") o.seg_rows = value < 0 ? 0 : value;
+    else if (n == "seam") o.seam = value < 0 ? -1 : 0;
+    else if (n == "ragged_stream") o.ragged_stream = value != 0;
     else if (n == "coop_r") {
         if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
         o.coop_r = (int)value;
@@ -1154,6 +1205,8 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "wave_resident") *value = o.wave_resident;
     else if (n == "split") *value = o.split;
     else if (n == "seg_rows") *value = o.seg_rows;
+    else if (n == "seam") *value = o.seam;
+    else if (n == "ragged_stream") *value = o.ragged_stream;
     else if (n == "coop_r") *value = o.coop_r;
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
     else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
@@ -1177,13 +1230,19 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a{};
     a.words = s->width / 32;
+    a.pitch = s->pitch;
+    a.rows = s->rows;
+    a.ghost = s->ghost;
+    a.y0 = s->y0;
+    a.height = s->height;
     a.out_begin = out_begin;
     a.out_end = out_end;
     a.ilv = s->ilv;
+    a.spare = s->spare_waves > 0 ? s->spare_waves : 0;
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
     if (waves)
-        *waves = a.nstrips * a.nsegs *
+        *waves = (a.nstrips * a.nsegs + a.rem_units) *
                  (a.split > 0 ? gol::stream_wpb(a.words, k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
     return GOL_OK;
 }

@@ -24,15 +24,27 @@ struct StreamArgs {
     int32_t spare;      // waves to leave free for concurrent launches (plan_stream)
     int32_t split_opt;  // 0: the engine's pair split; > 0: this split (1/65536); < 0: none (board option "split")
     int64_t seg_opt;    // 0: plan the segment length; > 0: rows per segment (board option "seg_rows")
+    // Seam geometry (torus, filled by plan_stream; gol_step.hip): `nstrips` strips of 63 stored blocks plus one seam
+    // lane holding both halos, and the rem = nblocks - 63 * nstrips blocks left over in remainder waves that pack
+    // rem_p sub-strips of (rem + 2) lanes, each on its own row segment.
+    int32_t seam;       // 1: seam geometry; 0: strips of 62 stored blocks with a halo lane on each side
+    int32_t rem;        // remainder blocks per row (0..62)
+    int32_t rem_p;      // remainder sub-strips per wave
+    int64_t rem_units;  // remainder units (after the nstrips * nsegs main units)
+    int64_t rem_mid;    // segments 1 .. rem_mid share remainder waves (the others have one each)
+    int32_t seam_opt;   // board option "seam": 0 = the engine's choice, < 0 = off
+    int32_t rag_bits;   // ragged rows (width not a multiple of 32): cells in a row's last word (1..31); 0 otherwise
+    int32_t rag_origin; // filled by plan_stream: ragged torus strips start at ring position -rag_origin
 };
 
 // ---- gol_step.hip
 bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
-int64_t stream_strips(int64_t words, int ilv, int k, bool bounded);
+// rag_bits: cells in the last word of a ragged row (words = ceil(W / 32), ilv 1), 0 for whole-word rows
+int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0);
 int stream_pair_split(int k, int ilv, bool bounded);
-int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap);
+int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits = 0);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,

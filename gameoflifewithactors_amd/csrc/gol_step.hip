@@ -32,6 +32,7 @@ namespace gol {
 
 static constexpr int kWave = 64;
 static constexpr int kInterior = kWave - 2;  // blocks stored per wave column strip (deep passes)
+static constexpr int kSeamInterior = kWave - 1;  // ... per seam strip (torus: one lane holds both halos)
 // 8 waves per workgroup: the deep passes run 2-3 waves per SIMD, so a workgroup spans the CU's SIMDs
 // twice (profiles/r1/ab_fence2.log: +3-6 % at K = 16 / 32 over 4-wave workgroups)
 #ifndef GOL_WAVES_PER_BLOCK
@@ -54,11 +55,18 @@ struct Wpb {
 // Block-edge words of the neighbouring lanes, by DPP (a half-rate VALU move on gfx950,
 // profiles/r1/valu_rates_gfx950.jsonl).  ds_bpermute_b32 in either direction measured 2-17 % slower under
 // the level-fenced schedule below (its ~60-cycle latency; profiles/r1/ab_xlane2.log).
+// ROT (torus): rotates, so lane 0's left neighbour is lane 63 -- the seam lane of a seam strip, a halo lane (whose
+// outer edge is garbage anyway) otherwise.  Bounded boards shift with zero fill: the dead cells beyond the
+// board's edge in the edge-fill strips.
+template <bool ROT>
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i-1
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);  // wave_shr:1
+    if (ROT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);              // wave_shr:1
 }
+template <bool ROT>
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);  // wave_shl:1
+    if (ROT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);              // wave_shl:1
 }
 
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
@@ -160,20 +168,48 @@ struct StreamWave {
     // dword load per row; lanes 1-62 reload their own word, an L1 hit).  Stores are then whole
     // 64-block runs: 256 / 512 / 1024 B aligned, instead of 62-block runs at 248 B offsets
     // (profiles/r1/k1_nohalo_ab.log: 3.9-4.1 -> 4.7-5.1 TB/s).
-    static constexpr bool kNoHalo = K == 1;
+    // RAGGED torus rows (NARROW on a torus; M = 1): the width is not a multiple of 32.  Scratch rows of
+    // ceil(W / 32) words hold the cells, the last word partial (a.rag_bits cells), and the row is a ring of W cells
+    // (GameOfLifeDriver.fs:21-25): the lane holding word 0 takes its west carry from bit rag_bits - 1 of the word
+    // before it, the lane holding the last word its east carry at bit rag_bits - 1 from the word after it, and the
+    // last word's bits past the row are cleared every generation (DESIGN.md 4.1 "Ragged rows").
+    static constexpr bool kRagged = !BOUNDED && NARROW;
+    static_assert(!kRagged || (M == 1 && WRAP_ROWS), "ragged rows: single boards of consecutive words");
+    static constexpr bool kNoHalo = K == 1 && !kRagged;
     static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
-    // per-lane column masks: narrow bounded boards, and the K = 1 halo-free strips (their last strip may end
-    // past the board's last block)
+    // per-lane column masks: narrow (or ragged) bounded boards, and the K = 1 halo-free strips (their last strip
+    // may end past the board's last block)
     static constexpr bool kColMask = BOUNDED && (NARROW || kNoHalo);
-    static_assert(BOUNDED || !NARROW, "NARROW is a bounded-board variant");
+
+    // Seam strips (torus deep passes, a.seam): lanes 0..62 hold 63 consecutive blocks and all store; lane 63, the
+    // SEAM lane, holds the first half of the block right of lane 62 (bits 0..15 of its words: cells 0..16M-1 of
+    // the interleaved block) and the second half of the block left of lane 0 (bits 16..31).  With rotating DPP
+    // moves the row is then a ring whose only break is in the middle of the seam lane, and the wrong cells the
+    // break produces spread one cell per generation: after K <= 16M generations they have not reached either
+    // end of the seam lane, so lanes 0..62 are exact.  One halo lane per wave instead of two: a 65536-cell row
+    // at M = 2 is 16 seam strips plus 16 blocks, against 17 strips of 62 (DESIGN.md 4.1 "Seam strips").
+    static constexpr bool kSeam = !BOUNDED && !(K == 1) && !kRagged;
+    // Deep passes (K > 1) stage their prefetched rows through LDS (see `stage` below); the K = 1 pass keeps two
+    // register buffers (it has registers to spare, and its halo-free strips load a neighbour word per row).
+    static constexpr bool kStage = !kNoHalo;
 
     const uint32_t* __restrict__ src;
     uint32_t* __restrict__ dst;
     const StreamArgs& a;
-    int load_off;      // this lane's byte offset in a row (its block column)
+    int load_off;      // this lane's byte offset in a row (its block column; remainder waves: plus its sub-strip's rows)
     int store_off;     // = load_off for interior on-board lanes, kNoStore otherwise
     uint32_t colmask;  // kColMask: ~0 for an on-board block
     int64_t row_bytes;
+    int64_t span_bytes;  // bytes a row descriptor covers: the row, or (remainder waves) every sub-strip's row
+    // kStage: rows are prefetched straight to LDS (buffer_load_dword ... lds), not to registers: a second prefetch
+    // buffer of R x M VGPRs -- with the seam lane's extra half-block -- spilled the (12, 2) pass at its 168-VGPR
+    // budget.  The trip reads its rows back at its top, after the wait, so a bounded board's row masks apply there
+    // and never make a trip wait for its own prefetch.  kSeam: per row and word a second dword load lands in the
+    // stage, the word at seam_off -- for the seam lane the block left of lane 0, for every other lane its own word
+    // again (a cache hit) -- and each lane takes the high half of its word from it: a no-op except on the seam lane.
+    int seam_off = 0;
+    using Stage = uint32_t[2][kSeam ? 2 : 1][R][M][kWave];  // [prefetch parity][row word, seam word][row][word][lane]
+    Stage* stage = nullptr;
     int64_t seg_begin, seg_end, nsteps, ly0;
     int64_t load_br;  // wrap: buffer row of the next level-0 row to load; else buffer row of step 0 (uniform)
     int seglen = 0, step_lo = 0, step_hi = 0, mrow_lo = 0, mrow_hi = 0;
@@ -192,6 +228,9 @@ struct StreamWave {
     // K = 1 halo-free strips: byte offset of this lane's neighbour word, and its bounded-board mask
     int nb_off = 0;
     uint32_t nbmask = 0xffffffffu;
+    // kRagged: west carry shift (32 - rag_bits on the lane holding word 0), east carry position (rag_bits - 1 on
+    // the lane holding the last word, else 31) and the cells of the lane's word on the row
+    uint32_t rag_shw = 0, rag_she = 31, rag_mask = 0xffffffffu;
 
     // First row (relative to the group segment of `len` rows) of the i-th oldest wave's share.  Shares
     // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
@@ -215,10 +254,14 @@ struct StreamWave {
 
     // `lane`: lane within the wave's strip.  `role`: -1 = the wave owns segment sy; 0, 1, ... = the
     // oldest, next, ... wave of the SIMD group sharing group segment sy (split by a.split, see plan_stream)
+    // `rem_count` > 0: a remainder wave of the seam geometry whose lanes hold rem_count sub-strips of (a.rem + 2)
+    // lanes, sub-strip j on segment sy + j (all of length a.seg); 0: a strip sx of segment sy.
     __device__ __forceinline__ StreamWave(const uint32_t* s, uint32_t* d, const StreamArgs& args, int lane,
-                                          int64_t sx, int64_t sy, int role = -1)
+                                          int64_t sx, int64_t sy, int role = -1, int rem_count = 0)
         : src(s), dst(d), a(args) {
         const int64_t nblocks = a.words / M;
+        row_bytes = a.words * 4;
+        span_bytes = row_bytes;
         // Bounded boards at least a strip wide (edge-fill strips): the first strip starts at the board's first
         // block and the last ends at its last block, so the dead cells beyond the left / right edge arrive as
         // the zeros the DPP moves write into lanes 0 / 63 (bound_ctrl), and no lane is ever off the board --
@@ -233,7 +276,21 @@ struct StreamWave {
         if (BOUNDED) {
             const bool in = cb >= 0 && cb < nblocks;
             colmask = in ? 0xffffffffu : 0u;
+            // a ragged bounded row's last word: only its first rag_bits cells are on the board (Script.fsx:6-13)
+            if (a.rag_bits && cb == nblocks - 1) colmask = (1u << a.rag_bits) - 1u;
             lc = in ? cb : 0;
+        } else if (kRagged) {
+            // strips of 62 stored words over the ring positions -o .. nw - 1 - o (o = a.rag_origin: 1, or 2 when
+            // the last strip's right halo lane would be the partial word), so the partial word is never a halo
+            // lane next to a stored lane (its few cells could not carry a K-deep halo): strip sx, lane l holds
+            // position 62 sx + l - 1 - o
+            const int64_t p = sx * kInterior + lane - 1 - a.rag_origin;
+            lc = floor_mod(p, nblocks);
+            colmask = 0xffffffffu;
+            cb = p;
+            rag_shw = lc == 0 ? 32u - (uint32_t)a.rag_bits : 0u;
+            rag_she = lc == nblocks - 1 ? (uint32_t)a.rag_bits - 1u : 31u;
+            rag_mask = lc == nblocks - 1 ? (1u << a.rag_bits) - 1u : 0xffffffffu;
         } else {
             colmask = 0xffffffffu;
             lc = floor_mod(cb, nblocks);
@@ -256,10 +313,32 @@ struct StreamWave {
             nb_off = (int)((nl * M + nbw) * 4);
         } else if (BOUNDED && edge_fill) {  // lane 0 is a halo lane unless it is the board's first block, lane 63 unless the last
             store_off = ((lane >= 1 || sx == 0) && (lane <= kInterior || sx == a.nstrips - 1)) ? load_off : kNoStore;
+        } else if (kRagged) {
+            store_off = (lane >= 1 && lane <= kInterior && cb <= nblocks - 1 - a.rag_origin) ? load_off : kNoStore;
         } else {
             store_off = (lane >= 1 && lane <= kInterior && cb < nblocks) ? load_off : kNoStore;
         }
-        row_bytes = a.words * 4;
+        if constexpr (kSeam) {
+            if (a.seam && rem_count == 0) {  // seam strip sx: blocks 63 sx .. 63 sx + 62, then the seam lane
+                const int64_t b = sx * kSeamInterior + lane;
+                if (lane < kSeamInterior) {
+                    load_off = store_off = (int)(floor_mod(b, nblocks) * 4 * M);
+                } else {
+                    load_off = (int)(floor_mod(b, nblocks) * 4 * M);                          // right of lane 62
+                    seam_off = (int)(floor_mod(sx * kSeamInterior - 1, nblocks) * 4 * M);     // left of lane 0
+                    store_off = kNoStore;
+                }
+            } else if (a.seam) {  // remainder wave: sub-strip j = lane / (rem + 2) on segment sy + j
+                const int q = a.rem + 2;
+                const int j = lane / q, i = lane - j * q;
+                const int64_t b = a.nstrips * kSeamInterior - 1 + i;  // halo, the rem remainder blocks, halo
+                const int64_t delta = (int64_t)j * a.seg * a.pitch * 4;  // this sub-strip's rows (bytes)
+                load_off = (int)(floor_mod(b, nblocks) * 4 * M + (j < rem_count ? delta : 0));
+                store_off = (j < rem_count && i >= 1 && i <= a.rem) ? load_off : kNoStore;
+                span_bytes = (int64_t)(rem_count - 1) * a.seg * a.pitch * 4 + row_bytes;
+            }
+            if (lane < kSeamInterior || !a.seam || rem_count) seam_off = load_off;
+        }
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
         if (role >= 0) {  // group segment: wave `role` (0 = oldest) takes its share, in age order
@@ -309,8 +388,9 @@ struct StreamWave {
             for (int j = 0; j < M; j++) sX[g][j] = cX[g][j] = sY[g][j] = cY[g][j] = aY[g][j] = 0;
     }
 
-    // Load the next R level-0 rows.  Loads are unconditional (addresses clamped, values masked) so every
-    // trip issues a fixed number of memory operations and the compiler waits for exactly the loads.
+    // Load the next R level-0 rows into `buf` (bounded boards and the K = 1 pass).  Loads are unconditional
+    // (addresses clamped, values masked) so every trip issues a fixed number of memory operations and the compiler
+    // waits for exactly the loads.
     __device__ __forceinline__ void load(uint32_t (&buf)[R][M], uint32_t (&nb)[R], int64_t first_step) {
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -330,7 +410,7 @@ struct StreamWave {
                 load_br = br + 1;
                 br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
-            V::load(row_rsrc(src + br * a.pitch, row_bytes), load_off, buf[r]);
+            V::load(row_rsrc(src + br * a.pitch, span_bytes), load_off, buf[r]);
             if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
             if (BOUNDED) {
                 const uint32_t rm = row_mask((int)first_step + r);
@@ -348,6 +428,57 @@ struct StreamWave {
         return (st >= mrow_lo && st < mrow_hi) ? 0xffffffffu : 0u;
     }
 
+    // kStage: prefetch the next R level-0 rows (steps first_step ..) into stage parity PAR (the row walk of load():
+    // wrap inside a single board, clamp to a ghost-row strip's buffer, clamp to a bounded board's buffer).
+    template <int PAR>
+    __device__ __forceinline__ void stage_load(int64_t first_step) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            int64_t br = load_br;
+            if (WRAP_ROWS) {
+                load_br = br + 1 == a.rows ? 0 : br + 1;
+            } else if (BOUNDED) {
+                int st = (int)first_step + r;
+                st = st < step_lo ? step_lo : (st > step_hi ? step_hi : st);
+                br = load_br + st;
+            } else {
+                const int64_t buf_rows = a.rows + 2 * a.ghost;
+                load_br = br + 1;
+                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+            }
+            const __amdgpu_buffer_rsrc_t rs = row_rsrc(src + br * a.pitch, span_bytes);
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&(*stage)[PAR][0][r][j][0],
+                                                         4, load_off + 4 * j, 0, 0, 0);
+                if constexpr (kSeam)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&(*stage)[PAR][kSeam ? 1 : 0][r][j][0],
+                                                             4, seam_off + 4 * j, 0, 0, 0);
+            }
+        }
+    }
+    // kStage, after the wait for stage parity PAR: the trip's rows (steps first_step ..).  kSeam: each word's high half
+    // from the seam word.  Bounded: rows off the board (and, NARROW, columns off it) are dead (Script.fsx:11).
+    template <int PAR>
+    __device__ __forceinline__ void stage_in(uint32_t (&v)[R][M], int lane, int64_t first_step) {
+        (void)first_step;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            [[maybe_unused]] uint32_t rm = 0xffffffffu;
+            if constexpr (BOUNDED) rm = row_mask((int)first_step + r);
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                const uint32_t x = (*stage)[PAR][0][r][j][lane];
+                if constexpr (kSeam)
+                    v[r][j] = lut3<0xD8>(0xffff0000u, (*stage)[PAR][kSeam ? 1 : 0][r][j][lane], x);
+                else if constexpr (BOUNDED)
+                    v[r][j] = kColMask ? lut3<0x80>(x, colmask, rm) : x & rm;
+                else
+                    v[r][j] = x;
+            }
+        }
+    }
+
     // One level, one row: window (prev P, centre C) + new row v -> next generation of the C row.
     // The new row's sums overwrite the P slot (it becomes the centre slot of the following row).
     template <bool MASK>
@@ -356,10 +487,18 @@ struct StreamWave {
                                               const uint32_t (&sC)[M], const uint32_t (&cC)[M],
                                               const uint32_t (&alC)[M], uint32_t rowmask, uint32_t (&out)[M]) {
         uint32_t sN[M], cN[M];
-        row_sum_block<M>(v, left, right, sN, cN);
+        if constexpr (kRagged) {  // the ring closes at bit level between the last word and word 0
+            const uint32_t w = align_right(v[0], left << rag_shw, 31);
+            const uint32_t e = (right << rag_she) | (v[0] >> 1);  // v[0]'s bits past the row are clear
+            sN[0] = lut3<0x96>(w, v[0], e);
+            cN[0] = lut3<0xE8>(w, v[0], e);
+        } else {
+            row_sum_block<M>(v, left, right, sN, cN);
+        }
 #pragma unroll
         for (int j = 0; j < M; j++) {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
+            if (kRagged) out[j] &= rag_mask;
             if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask, rowmask) : out[j] & rowmask;  // dead off the board
             sP[j] = sN[j];
             cP[j] = cN[j];
@@ -403,7 +542,7 @@ struct StreamWave {
         // it 213, 2 waves/SIMD; profiles/r1/ab_early.log, ab_fence2.log).
         uint32_t right[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) right[r] = from_right(v[r][0]);
+        for (int r = 0; r < R; r++) right[r] = from_right<!BOUNDED>(v[r][0]);
 #pragma unroll
         for (int g = 0; g < K; g++) {
             if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
@@ -416,9 +555,9 @@ struct StreamWave {
                 }
                 // even row: window (X = row-2, Y = row-1) -> X;  odd row: (Y, X) -> Y
                 uint32_t o0[M], o1[M];
-                level_row<MASK>(v[r], from_left(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
-                level_row<MASK>(v[r + 1], from_left(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g], v[r], m1,
-                          o1);
+                level_row<MASK>(v[r], from_left<!BOUNDED>(v[r][M - 1]), right[r], sX[g], cX[g], sY[g], cY[g], aY[g], m0, o0);
+                level_row<MASK>(v[r + 1], from_left<!BOUNDED>(v[r + 1][M - 1]), right[r + 1], sY[g], cY[g], sX[g], cX[g],
+                                v[r], m1, o1);
 #pragma unroll
                 for (int j = 0; j < M; j++) {
                     aY[g][j] = v[r + 1][j];
@@ -426,8 +565,8 @@ struct StreamWave {
                     v[r + 1][j] = o1[j];
                 }
                 if (g + 1 < K) {
-                    right[r] = from_right(o0[0]);
-                    right[r + 1] = from_right(o1[0]);
+                    right[r] = from_right<!BOUNDED>(o0[0]);
+                    right[r + 1] = from_right<!BOUNDED>(o1[0]);
                     __builtin_amdgcn_sched_barrier(kAllButDs);
                 }
             }
@@ -436,7 +575,7 @@ struct StreamWave {
     }
 
     __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
-        V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? row_bytes : 0), store_off, v);
+        V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? span_bytes : 0), store_off, v);
     }
     // Store trip t's outputs.  Rows outside the segment (pipeline fill and the tail) get an empty
     // descriptor (num_records 0): the stores are dropped by the range check with no branch, and the row
@@ -481,19 +620,36 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     // wave index made provably uniform so all row bookkeeping lives in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     constexpr int WPB = Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value;
+    int64_t unit;  // a strip's segment (or SIMD group segment), then the seam geometry's remainder units
     if (a.split > 0) {  // waves w, w + 4, ... share a SIMD: one group segment between them
-        const int64_t group = (int64_t)blockIdx.x * 4 + (wave & 3);
+        unit = (int64_t)blockIdx.x * 4 + (wave & 3);
         role = wave >> 2;  // 0 = the oldest
-        if (group >= a.nstrips * a.nsegs) return;
-        sx = group % a.nstrips;
-        sy = group / a.nstrips;
     } else {
-        const int64_t gw = (int64_t)blockIdx.x * WPB + wave;
-        if (gw >= a.nstrips * a.nsegs) return;
-        sx = gw % a.nstrips;
-        sy = gw / a.nstrips;
+        unit = (int64_t)blockIdx.x * WPB + wave;
     }
-    W w(src, dst, a, lane, sx, sy, role);
+    const int64_t main_units = a.nstrips * a.nsegs;
+    if (unit >= main_units + a.rem_units) return;
+    int rem_count = 0;
+    if (unit < main_units) {
+        sx = unit % a.nstrips;
+        sy = unit / a.nstrips;
+    } else {
+        // remainder unit r (seam geometry): segments 1 .. rem_mid, all of length a.seg and with every row they
+        // stream inside the board, rem_p at a time (sub-strip j = segment sy + j: a per-lane row offset); the
+        // others alone (the first segment's rows wrap or reach the ghost rows, the last is shorter)
+        const int64_t r = unit - main_units;
+        const int64_t packed = (a.rem_mid + a.rem_p - 1) / a.rem_p;
+        sx = a.nstrips;
+        if (r >= 1 && r <= packed) {
+            sy = 1 + (r - 1) * a.rem_p;
+            const int64_t left = 1 + a.rem_mid - sy;
+            rem_count = (int)(left < a.rem_p ? left : a.rem_p);
+        } else {
+            sy = r == 0 ? 0 : r - packed + a.rem_mid;
+            rem_count = 1;
+        }
+    }
+    W w(src, dst, a, lane, sx, sy, role, rem_count);
 #if GOL_STAMP
     const int64_t stamp_id = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t stamp_t0 = __builtin_amdgcn_s_memrealtime();
@@ -502,26 +658,85 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     const int64_t ntrips = (w.nsteps + R - 1) / R;
     const int64_t t_fill = (2 * K) / R < ntrips ? (2 * K) / R : ntrips;  // trips entirely before step 2K
 
-    // Trip t (rows of trip t in `cur`, trip t-1's outputs in `other`):
-    //   [wait for all memory ops of trip t-1] [store `other`] [prefetch trip t+1 into `other`]
-    //   [compute trip t in place in `cur`]
-    // Stores are deferred by one trip so the wait at the top never covers an operation issued less than
-    // a whole trip earlier (the wait-count pass treats pending loads and stores as completing out of
-    // order: waiting for a prefetched row with a younger store in flight would drain that store too),
-    // and the two row buffers alternate roles (A/B) so no register copy or early wait joins a prefetch.
-    uint32_t A[R][M], B[R][M], NA[R], NB[R];  // rows and (K = 1 halo-free) neighbour words
+    // Row buffers: B is the staged passes' one buffer; A / B alternate roles in the K = 1 pass.  NA / NB: the K = 1
+    // halo-free strips' neighbour words.  Stores are deferred by one trip in both (see the loops below).
+    uint32_t A[R][M], B[R][M], NA[R], NB[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
         NA[r] = NB[r] = 0;
 #pragma unroll
         for (int j = 0; j < M; j++) B[r][j] = 0;
     }
-    w.load(A, NA, 0);
+    if constexpr (!W::kStage) w.load(A, NA, 0);
     using Skip = std::true_type;
     using NoSkip = std::false_type;
+    using P0 = std::integral_constant<int, 0>;  // staged trips: read stage parity 0, prefetch into parity 1
+    using P1 = std::integral_constant<int, 1>;
     const int64_t fill_pairs = (t_fill < ntrips ? t_fill : ntrips) / 2;
     int64_t t = 0;
-    if constexpr (!BOUNDED) {
+    if constexpr (W::kStage) {
+        // Deep passes: one row buffer in registers, rows staged through LDS (stage_load / stage_in).  Trip t:
+        //   [wait for all memory ops of trip t-1] [store trip t-1's outputs] [read trip t's rows from the stage]
+        //   [prefetch trip t+1 into the other stage parity] [compute trip t in place]
+        // Stores are deferred by one trip so the wait at the top never covers an operation issued less than a whole
+        // trip earlier (the wait-count pass treats pending loads and stores as completing out of order).
+        __shared__ typename W::Stage stage[WPB];
+        w.stage = &stage[wave];
+        uint32_t NV[R];  // (K = 1 neighbour words: unused here)
+#pragma unroll
+        for (int r = 0; r < R; r++) NV[r] = 0;
+        w.template stage_load<0>(0);
+        auto trip = [&](int64_t tt, auto skip, auto mask, auto par) {
+            constexpr int PAR = decltype(par)::value;
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            w.store_masked(B, tt - 1);
+            w.template stage_in<PAR>(B, lane, tt * R);
+            w.template stage_load<1 - PAR>((tt + 1) * R);
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
+            w.template process<decltype(skip)::value, decltype(mask)::value>(B, NV, tt);
+        };
+        using Mask = std::true_type;
+        using NoMask = std::false_type;
+        if constexpr (!BOUNDED) {
+            for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
+                trip(t, Skip{}, NoMask{}, P0{});
+                trip(t + 1, Skip{}, NoMask{}, P1{});
+            }
+            for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
+                trip(t, NoSkip{}, NoMask{}, P0{});
+                trip(t + 1, NoSkip{}, NoMask{}, P1{});
+            }
+            if (t < ntrips) trip(t++, NoSkip{}, NoMask{}, P0{});
+        } else {
+            // Bounded board: the trips that produce rows off the board (the fill trips and, in the steady state,
+            // t < t_top or t >= t_bot: near the board's top and bottom edges) mask them dead at every level; the
+            // others run the unmasked arithmetic of the torus strips.
+            for (int64_t p = 0; p < fill_pairs; p++, t += 2) {
+                trip(t, Skip{}, Mask{}, P0{});
+                trip(t + 1, Skip{}, Mask{}, P1{});
+            }
+            for (; t + 1 < ntrips && t < w.t_top; t += 2) {
+                trip(t, NoSkip{}, Mask{}, P0{});
+                trip(t + 1, NoSkip{}, Mask{}, P1{});
+            }
+            const int64_t t_end = w.t_bot < ntrips ? w.t_bot : ntrips;
+            for (; t + 1 < t_end; t += 2) {
+                trip(t, NoSkip{}, NoMask{}, P0{});
+                trip(t + 1, NoSkip{}, NoMask{}, P1{});
+            }
+            for (; t + 1 < ntrips; t += 2) {
+                trip(t, NoSkip{}, Mask{}, P0{});
+                trip(t + 1, NoSkip{}, Mask{}, P1{});
+            }
+            if (t < ntrips) trip(t++, NoSkip{}, Mask{}, P0{});
+        }
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        w.store_masked(B, t - 1);
+    } else if constexpr (!BOUNDED) {
+        // K = 1 (rows of trip t in `cur`, trip t-1's outputs in `other`):
+        //   [wait for all memory ops of trip t-1] [store `other`] [prefetch trip t+1 into `other`]
+        //   [compute trip t in place in `cur`]
+        // the two row buffers alternate roles (A/B) so no register copy or early wait joins a prefetch.
         auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
                         int64_t tt, auto skip) {
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
@@ -530,11 +745,11 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
             w.template process<decltype(skip)::value, false>(cur, ncur, tt);
         };
-        for (int64_t p = 0; p < fill_pairs; p++, t += 2) {  // pipeline fill: all-garbage levels skipped
+        for (int64_t p = 0; p < fill_pairs; p++, t += 2) {
             trip(A, B, NA, NB, t, Skip{});
             trip(B, A, NB, NA, t + 1, Skip{});
         }
-        for (; t + 1 < ntrips; t += 2) {  // steady state (the odd fill / transition trip runs here unskipped)
+        for (; t + 1 < ntrips; t += 2) {
             trip(A, B, NA, NB, t, NoSkip{});
             trip(B, A, NB, NA, t + 1, NoSkip{});
         }
@@ -547,38 +762,25 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             w.store_masked(B, t - 1);
         }
     } else {
-        // Bounded board: the trips that produce rows off the board (the fill trips and, in the steady state,
-        // t < t_top or t >= t_bot: near the board's top and bottom edges) mask them dead at every level; the
-        // others run the unmasked arithmetic of the torus strips.
+        // K = 1 on a bounded board: every trip masks (halo-free strips carry per-lane column masks)
         auto trip = [&](uint32_t (&cur)[R][M], uint32_t (&other)[R][M], uint32_t (&ncur)[R], uint32_t (&nother)[R],
-                        int64_t tt, auto skip, auto mask) {
+                        int64_t tt, auto skip) {
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             w.store_masked(other, tt - 1);
             w.load(other, nother, (tt + 1) * R);
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
-            w.template process<decltype(skip)::value, decltype(mask)::value>(cur, ncur, tt);
+            w.template process<decltype(skip)::value, true>(cur, ncur, tt);
         };
-        using Mask = std::true_type;
-        using NoMask = std::false_type;
         for (int64_t p = 0; p < fill_pairs; p++, t += 2) {
-            trip(A, B, NA, NB, t, Skip{}, Mask{});
-            trip(B, A, NB, NA, t + 1, Skip{}, Mask{});
-        }
-        for (; t + 1 < ntrips && t < w.t_top; t += 2) {
-            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
-            trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
-        }
-        const int64_t t_end = w.t_bot < ntrips ? w.t_bot : ntrips;
-        for (; t + 1 < t_end; t += 2) {
-            trip(A, B, NA, NB, t, NoSkip{}, NoMask{});
-            trip(B, A, NB, NA, t + 1, NoSkip{}, NoMask{});
+            trip(A, B, NA, NB, t, Skip{});
+            trip(B, A, NB, NA, t + 1, Skip{});
         }
         for (; t + 1 < ntrips; t += 2) {
-            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
-            trip(B, A, NB, NA, t + 1, NoSkip{}, Mask{});
+            trip(A, B, NA, NB, t, NoSkip{});
+            trip(B, A, NB, NA, t + 1, NoSkip{});
         }
         if (t < ntrips) {
-            trip(A, B, NA, NB, t, NoSkip{}, Mask{});
+            trip(A, B, NA, NB, t, NoSkip{});
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             w.store_masked(A, t);
         } else {
@@ -620,18 +822,26 @@ int stream_largest_k(int64_t n, int cap, int ilv) {
     return 1;
 }
 
-// A bounded board narrower than one wave strip takes the column-masked variant (StreamWave NARROW).
-static bool stream_narrow(int64_t words, int ilv, int k, bool bounded) {
-    return bounded && k > 1 && words / ilv < kWave;
+// The NARROW template flag: on a bounded board the column-masked variant, for boards narrower than one wave strip and
+// for ragged rows (rag_bits: cells in a ragged row's last word); on a torus the ragged-row variant (StreamWave
+// kRagged).
+static bool stream_narrow(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0) {
+    if (!bounded) return rag_bits != 0;
+    return k > 1 && (words / ilv < kWave || rag_bits != 0);
 }
 
-// Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, bounded
-// (never wraps: rows beyond the board are masked dead; narrow boards mask columns too).
+// Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, ragged torus rows
+// (single board, ilv 1), bounded (never wraps: rows beyond the board are masked dead; narrow and ragged boards
+// mask columns too).
 template <int K, int M>
 static const void* stream_kernel(bool bounded, bool wrap, bool narrow) {
     if (bounded)
         return narrow ? (const void*)&gol_stream_step<K, M, true, false, true>
                       : (const void*)&gol_stream_step<K, M, true, false, false>;
+    if (narrow) {
+        if constexpr (M == 1) return wrap ? (const void*)&gol_stream_step<K, 1, false, true, true> : nullptr;
+        return nullptr;
+    }
     return wrap ? (const void*)&gol_stream_step<K, M, false, true, false>
                 : (const void*)&gol_stream_step<K, M, false, false, false>;
 }
@@ -644,8 +854,9 @@ static const void* kernel_for(int k, int ilv, bool bounded, bool wrap, bool narr
     return nullptr;
 }
 
-int64_t stream_strips(int64_t words, int ilv, int k, bool bounded) {
+int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits) {
     const int64_t nblocks = words / ilv;
+    if (rag_bits && !bounded) return (nblocks + kInterior - 1) / kInterior;  // ragged torus rows: see plan_stream
     if (k == 1) return (nblocks + kWave - 1) / kWave;  // K = 1: halo-free strips
     // bounded edge-fill strips (StreamWave::edge_fill): strip 0 stores blocks [0, 63), strip s stores
     // [62 s + 1, 62 s + 63), the last ends at the board's last block
@@ -654,12 +865,13 @@ int64_t stream_strips(int64_t words, int ilv, int k, bool bounded) {
 }
 
 // Waves per workgroup of a variant (Wpb)
-int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap) {
-    const bool narrow = stream_narrow(words, ilv, k, bounded);
+int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits) {
+    const bool narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
 #define GOL_WPBQ(K_, M_)                                                                                 \
     if (k == K_ && ilv == M_)                                                                            \
         return bounded ? (narrow ? Wpb<K_, M_, true, false, true>::value : Wpb<K_, M_, true, false, false>::value) \
-                       : (wrap ? Wpb<K_, M_, false, true, false>::value : Wpb<K_, M_, false, false, false>::value);
+                       : (narrow ? Wpb<K_, M_, false, true, true>::value                                  \
+                                 : (wrap ? Wpb<K_, M_, false, true, false>::value : Wpb<K_, M_, false, false, false>::value));
     GOL_FOR_EACH_KM(GOL_WPBQ)
 #undef GOL_WPBQ
     return kWavesPerBlock;
@@ -687,16 +899,16 @@ int stream_pair_split(int k, int ilv, bool bounded) {
 
 // Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.  Falls back
 // to 4096 waves when no device answers (host-only planning, e.g. CPU tests).
-static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool wrap) {
+static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits) {
     static std::atomic<int64_t> cache[33][5][2][2][2];
     const int64_t fallback = 4096;
     if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return fallback;
     if (bounded) wrap = false;
-    const bool narrow = stream_narrow(words, ilv, k, bounded);
+    const bool narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
     int64_t v = cache[k][ilv][bounded][wrap][narrow].load(std::memory_order_relaxed);
     if (v > 0) return v;
     const void* fn = kernel_for(k, ilv, bounded, wrap, narrow);
-    const int wpb = stream_wpb(words, k, ilv, bounded, wrap);
+    const int wpb = stream_wpb(words, k, ilv, bounded, wrap, rag_bits);
     const int threads = kWave * wpb;
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
@@ -711,14 +923,43 @@ static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool 
     return v;
 }
 
+// Remainder units of the seam geometry for nsegs segments (kernel: the unit mapping in gol_stream_step).
+static int64_t seam_rem_units(const StreamArgs& a, int64_t nsegs, int64_t rem_mid) {
+    if (!a.seam || a.rem == 0 || nsegs <= 0) return 0;
+    return 1 + (rem_mid + a.rem_p - 1) / a.rem_p + (nsegs - 1 - rem_mid);
+}
+
+// Does the seam geometry apply?  Torus deep passes (the bounded edge-fill strips keep their zero-fill edges) on rows
+// of at least one seam strip, with K <= 16 M (the break in the middle of the seam lane must not reach its ends).
+static bool seam_applies(const StreamArgs& a, int k, bool bounded) {
+    return a.seam_opt >= 0 && !bounded && !a.rag_bits && k > 1 && k <= 16 * a.ilv && a.words / a.ilv >= kSeamInterior;
+}
+
 // Work decomposition: nstrips column strips x nsegs row segments, one wave each (or one SIMD group of
-// waves per segment with the pair split).  The segment count makes the grid ONE balanced round of
-// resident waves (a partial second round would leave a tail of lone waves), with segments no shorter than
-// 2K rows (pipeline fill cost).  a.split_opt / a.seg_opt (a board's "split" / "seg_rows" options) override
-// the split and the segment length for experiments.
+// waves per segment with the pair split), plus the seam geometry's remainder units.  The segment count makes the
+// grid ONE balanced round of resident waves (a partial second round would leave a tail of lone waves), with
+// segments no shorter than 2K rows (pipeline fill cost).  a.split_opt / a.seg_opt / a.seam_opt (a board's "split" /
+// "seg_rows" / "seam" options) override the split, the segment length and the geometry for experiments.
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded));
-    a.nstrips = stream_strips(a.words, a.ilv, k, bounded);
+    const int64_t nblocks = a.words / a.ilv;
+    a.seam = seam_applies(a, k, bounded) ? 1 : 0;
+    a.rem = 0;
+    a.rem_p = 1;
+    a.rem_units = 0;
+    a.rem_mid = 0;
+    if (a.seam) {
+        a.nstrips = nblocks / kSeamInterior;
+        a.rem = (int32_t)(nblocks - a.nstrips * kSeamInterior);
+        a.rem_p = a.rem ? (kWave / (a.rem + 2) > 0 ? kWave / (a.rem + 2) : 1) : 1;
+    } else {
+        a.nstrips = stream_strips(a.words, a.ilv, k, bounded, a.rag_bits);
+    }
+    // Ragged torus rows (StreamWave kRagged): the strips start at ring position -1 (the partial last word, then word
+    // 0, ...), unless the last strip's right halo lane would then be the partial word next to a stored word; then
+    // at position -2.
+    a.rag_origin = 1;
+    if (a.rag_bits && !bounded && (a.nstrips * kInterior - 1 + 1) % nblocks == 0) a.rag_origin = 2;
     const int64_t rows = a.out_end - a.out_begin;
     if (rows <= 0) {
         a.nsegs = 0;
@@ -727,15 +968,18 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     }
     // a launch too short for one full group segment per strip (e.g. a k-row halo band) runs one wave per
     // segment: splitting a handful of rows only multiplies the pipeline fill
-    const int wpb = stream_wpb(a.words, k, a.ilv, bounded, wrap);
+    const int wpb = stream_wpb(a.words, k, a.ilv, bounded, wrap, a.rag_bits);
     if (a.split && rows < (int64_t)(wpb / 4) * (2 * k > 16 ? 2 * k : 16)) a.split = 0;
+    const int group = a.split ? wpb / 4 : 1;  // waves per segment
     int64_t seg = a.seg_opt;
+    int64_t slots = 0;
     if (seg <= 0) {
-        const int group = a.split ? wpb / 4 : 1;  // waves per segment
-        int64_t units = resident_units(a.words, k, a.ilv, bounded, wrap);
+        int64_t units = resident_units(a.words, k, a.ilv, bounded, wrap, a.rag_bits);
         if (a.spare > 0) units = units > a.spare + 1 ? units - a.spare : 1;
-        const int64_t slots = units / group;
-        int64_t nsegs = slots / a.nstrips;
+        slots = units / group;
+        // waves per segment: the strips, plus (seam geometry) a 1/rem_p share of a remainder wave
+        const double per_seg = (double)a.nstrips + (a.seam && a.rem ? 1.0 / a.rem_p : 0.0);
+        int64_t nsegs = (int64_t)((double)slots / per_seg);
         if (nsegs < 1) nsegs = 1;
         int64_t min_seg = (2 * k > 16 ? 2 * k : 16) * group;
         // A launch too small to fill a quarter of the device is latency-bound: each wave is one serial
@@ -750,20 +994,39 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
     if (seg > ((int64_t)1 << 30)) seg = (int64_t)1 << 30;  // the kernel counts a segment's rows in 32 bits
     a.seg = seg;
     a.nsegs = (rows + seg - 1) / seg;
+    if (a.seam && a.rem) {
+        // the per-lane row offsets of a packed remainder wave are 32-bit byte offsets into one descriptor
+        const int64_t row_bytes = a.words * 4, step = seg * (a.pitch > 0 ? a.pitch : a.words) * 4;
+        const int64_t fit = 1 + ((((int64_t)1 << 31) - 1 - row_bytes) / step);
+        if (a.rem_p > fit) a.rem_p = (int32_t)(fit > 1 ? fit : 1);
+        // segments 1 .. rem_mid share remainder waves: every row they stream must lie in the board / buffer
+        // without a wrap (a single board's last segment shorter than k would push its neighbour's halo past it)
+        int64_t mid = a.nsegs - 2;
+        if (wrap && a.nsegs >= 3 && rows - (a.nsegs - 1) * seg < k) mid = a.nsegs - 3;
+        a.rem_mid = mid > 0 ? mid : 0;
+        a.rem_units = seam_rem_units(a, a.nsegs, a.rem_mid);
+    }
 }
 
 template <int K, int M>
 static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs& a, bool bounded, bool wrap,
                             hipStream_t s) {
-    const int WPB = stream_wpb(a.words, K, M, bounded, wrap);
-    const int64_t waves = a.nstrips * a.nsegs * (a.split ? WPB / 4 : 1);
+    const int WPB = stream_wpb(a.words, K, M, bounded, wrap, a.rag_bits);
+    const int64_t waves = (a.nstrips * a.nsegs + a.rem_units) * (a.split ? WPB / 4 : 1);
     const unsigned blocks = (unsigned)((waves + WPB - 1) / WPB);
     const dim3 block(kWave * WPB);
     if (bounded) {
-        if (stream_narrow(a.words, M, K, true))
+        if (stream_narrow(a.words, M, K, true, a.rag_bits))
             hipLaunchKernelGGL((gol_stream_step<K, M, true, false, true>), dim3(blocks), block, 0, s, src, dst, a);
         else
             hipLaunchKernelGGL((gol_stream_step<K, M, true, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+    } else if (a.rag_bits) {
+        if constexpr (M == 1) {
+            if (!wrap) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((gol_stream_step<K, 1, false, true, true>), dim3(blocks), block, 0, s, src, dst, a);
+        } else {
+            return hipErrorInvalidValue;
+        }
     } else {
         if (wrap)
             hipLaunchKernelGGL((gol_stream_step<K, M, false, true, false>), dim3(blocks), block, 0, s, src, dst, a);

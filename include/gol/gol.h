@@ -150,6 +150,7 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *   "split" 0 | n | -1           streaming pass: the oldest wave's share of a SIMD group segment in 1/65536
  *                                (0: the measured default, -1: no split)
  *   "seg_rows" 0 | n             streaming pass: rows per wave segment (0: planned)
+ *   "seam" 0 | -1                streaming pass on a torus: seam strips where they apply (-1: halo-lane strips)
  *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments
  *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
  *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)

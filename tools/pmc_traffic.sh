@@ -1,16 +1,23 @@
 #!/bin/bash
-# HBM-traffic PMC passes for the bench configuration (run on the GPU box from the repo root).
-# One counter per rocprofv3 pass (FETCH_SIZE and WRITE_SIZE cannot share one), each under its own
-# time limit; then the calibrated per-launch summary -> gpurun_out/pmc_traffic/pmc_traffic.json.
+# HBM-traffic PMC passes for one bench configuration (run on the GPU box from the repo root), each counter in its own
+# rocprofv3 pass under its own time limit, then the calibrated per-launch summary merged into
+#   gpurun_out/pmc_traffic/pmc_traffic.json  (copy to profiles/pmc_traffic.json)
+#   tools/pmc_traffic.sh [boundary] [k]      (default: torus 12)
 set -e
+boundary=${1:-torus}; k=${2:-12}
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-out=gpurun_out/pmc_traffic
+out=gpurun_out/pmc_traffic_${boundary}_k$k
 mkdir -p $out
-bench="python3 bench.py --no-cpu-baseline --steps 8 --warmup 1"
+steps=8
+bench="python3 bench.py --no-cpu-baseline --steps $steps --warmup 1 --tblock $k --boundary $boundary"
 calib=tools/ubench/traffic_calib
+[ -x $calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o $calib tools/ubench/traffic_calib.hip
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/calib_fetch -o run -- $calib > $out/calib_fetch.log 2>&1
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/calib_write -o run -- $calib > $out/calib_write.log 2>&1
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/bench_fetch -o run -- $bench > $out/bench_fetch.log 2>&1
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/bench_write -o run -- $bench > $out/bench_write.log 2>&1
-python3 tools/pmc_traffic.py $out ${1:-65536x65536_k12} ${2:-2} > $out/pmc_traffic.json
-cat $out/pmc_traffic.json
+merge=gpurun_out/pmc_traffic/pmc_traffic.json
+mkdir -p gpurun_out/pmc_traffic
+[ -f $merge ] || cp profiles/pmc_traffic.json $merge
+python3 tools/pmc_traffic.py $out 65536 65536 $boundary $k 2 $steps $merge > $merge.new && mv $merge.new $merge
+python3 -c "import json;d=json.load(open('$merge'));import sys;k=[x for x in d if x.endswith('_$boundary'+'_k$k'+'_m2') or '_${boundary}_k${k}_m2' in x];print({x:d[x]['bytes_per_launch'] for x in k})"

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--boundary", type=int, default=0)
     p.add_argument("--ilv", type=int, default=0, help="packed layout (0 = the engine default for the width)")
     p.add_argument("--split", type=float, default=None, help="board option 'split' (fraction; negative = off)")
+    p.add_argument("--seam", type=int, default=0, help="board option 'seam' (0 = engine choice, -1 = halo-lane strips)")
     a = p.parse_args()
     import torch
 
@@ -30,7 +31,7 @@ def main():
     H = a.height or a.size
     lib = _lib.load()
     ilv = a.ilv or lib.gol_default_ilv(W)
-    opts = {"coop": 0}
+    opts = {"coop": 0, "seam": a.seam}
     if a.split is not None:
         opts["split"] = int(a.split * 65536) if a.split >= 0 else -1
     for k in [int(x) for x in a.ks.split(",")]:
@@ -48,7 +49,7 @@ def main():
             b.synchronize()
             t = e0.elapsed_time(e1) / 1e3 / a.passes
             gcups = W * H * k / t / 1e9
-            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
+            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
                               "alg_GBps": round(W * H / 4 / t / 1e9, 1),
                               }), flush=True)
 
