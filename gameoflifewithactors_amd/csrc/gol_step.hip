@@ -457,24 +457,43 @@ struct StreamWave {
             }
         }
     }
-    // kStage, after the wait for stage parity PAR: the trip's rows (steps first_step ..).  kSeam: each word's high half
-    // from the seam word.  Bounded: rows off the board (and, NARROW, columns off it) are dead (Script.fsx:11).
+    // kStage, after the wait for stage parity PAR and the previous trip's stores: read the trip's words from the stage
+    // straight into the row buffer (and the seam words), before the next prefetch is issued, so the LDS latency
+    // hides behind it ...
+    struct Seam {
+        uint32_t s[kSeam ? R : 1][M];
+    };
     template <int PAR>
-    __device__ __forceinline__ void stage_in(uint32_t (&v)[R][M], int lane, int64_t first_step) {
+    __device__ __forceinline__ void stage_read(uint32_t (&v)[R][M], int lane) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int j = 0; j < M; j++) v[r][j] = (*stage)[PAR][0][r][j][lane];
+    }
+    template <int PAR>
+    __device__ __forceinline__ void stage_read_seam(Seam& t, int lane) {
+        if constexpr (kSeam) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int j = 0; j < M; j++) t.s[r][j] = (*stage)[PAR][kSeam ? 1 : 0][r][j][lane];
+        }
+    }
+    // ... and make them the rows of steps first_step ..: kSeam, each word's high half from the seam word; bounded, rows
+    // off the board (and, NARROW, columns off it) dead (Script.fsx:11).
+    __device__ __forceinline__ void stage_in(uint32_t (&v)[R][M], const Seam& t, int64_t first_step) {
         (void)first_step;
+        (void)t;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             [[maybe_unused]] uint32_t rm = 0xffffffffu;
             if constexpr (BOUNDED) rm = row_mask((int)first_step + r);
 #pragma unroll
             for (int j = 0; j < M; j++) {
-                const uint32_t x = (*stage)[PAR][0][r][j][lane];
                 if constexpr (kSeam)
-                    v[r][j] = lut3<0xD8>(0xffff0000u, (*stage)[PAR][kSeam ? 1 : 0][r][j][lane], x);
+                    v[r][j] = lut3<0xD8>(0xffff0000u, t.s[kSeam ? r : 0][j], v[r][j]);
                 else if constexpr (BOUNDED)
-                    v[r][j] = kColMask ? lut3<0x80>(x, colmask, rm) : x & rm;
-                else
-                    v[r][j] = x;
+                    v[r][j] = kColMask ? lut3<0x80>(v[r][j], colmask, rm) : v[r][j] & rm;
             }
         }
     }
@@ -690,8 +709,12 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             constexpr int PAR = decltype(par)::value;
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             w.store_masked(B, tt - 1);
-            w.template stage_in<PAR>(B, lane, tt * R);
+            w.template stage_read<PAR>(B, lane);
+            __builtin_amdgcn_sched_barrier(0);  // the row reads before the prefetch: their latency hides behind it
             w.template stage_load<1 - PAR>((tt + 1) * R);
+            typename W::Seam st;
+            w.template stage_read_seam<PAR>(st, lane);
+            w.stage_in(B, st, tt * R);
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
             w.template process<decltype(skip)::value, decltype(mask)::value>(B, NV, tt);
         };
@@ -860,7 +883,8 @@ int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits)
     if (k == 1) return (nblocks + kWave - 1) / kWave;  // K = 1: halo-free strips
     // bounded edge-fill strips (StreamWave::edge_fill): strip 0 stores blocks [0, 63), strip s stores
     // [62 s + 1, 62 s + 63), the last ends at the board's last block
-    if (bounded && nblocks >= kWave) return (nblocks - 1 + kInterior - 1) / kInterior;
+    if (bounded && nblocks >= kWave && !rag_bits) return (nblocks - 1 + kInterior - 1) / kInterior;
+    // halo-lane strips (torus; bounded NARROW: narrow or ragged rows): strip s stores blocks [62 s, 62 s + 62)
     return (nblocks + kInterior - 1) / kInterior;
 }
 
