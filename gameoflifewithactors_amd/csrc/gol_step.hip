@@ -208,9 +208,30 @@ struct StreamWave {
     // stage, the word at seam_off -- for the seam lane the block left of lane 0, for every other lane its own word
     // again (a cache hit) -- and each lane takes the high half of its word from it: a no-op except on the seam lane.
     int seam_off = 0;
-    using Stage = uint32_t[2][kSeam ? 2 : 1][R][M][kWave];  // [prefetch parity][row word, seam word][row][word][lane]
+    // M dword LDS-DMAs per row and kind.  (One dwordx3 DMA per row at M = 2 -- there is no dwordx2 form -- saves 8
+    // instructions per trip but strides the stage 12 bytes per lane: the LDS reads then need more address registers
+    // than the (12, 2) pass has, and it spilled.)
+    static constexpr int kDmaWords = 1;  // dwords per lane per DMA
+    static constexpr int kDmas = M;      // DMAs per row and kind
+    using Stage = uint32_t[2][kSeam ? 2 : 1][R][kDmas][kWave * kDmaWords];  // [parity][row, seam][row][dma][lane x words]
     Stage* stage = nullptr;
+    template <int WORDS>
+    __device__ __forceinline__ static void dma(__amdgpu_buffer_rsrc_t rs, uint32_t* lds, int off) {
+        auto* p = (__attribute__((address_space(3))) void*)lds;
+        if constexpr (WORDS == 3)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, p, 12, off, 0, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, p, 4, off, 0, 0, 0);
+    }
+    __device__ __forceinline__ uint32_t staged(int par, int kind, int r, int j, int lane) const {
+        return kDmas == 1 ? (*stage)[par][kind][r][0][lane * kDmaWords + j] : (*stage)[par][kind][r][j][lane];
+    }
     int64_t seg_begin, seg_end, nsteps, ly0;
+    // kStage walks, wave-uniform (SGPRs): a bounded board's next row to load (byte address and step index; rows
+    // outside [step_lo, step_hi] load nothing), and every variant's next output row to store (byte address and step
+    // relative to seg_begin)
+    uint64_t lptr = 0, sptr = 0;
+    int lrow = 0, sd = 0;
     int64_t load_br;  // wrap: buffer row of the next level-0 row to load; else buffer row of step 0 (uniform)
     int seglen = 0, step_lo = 0, step_hi = 0, mrow_lo = 0, mrow_hi = 0;
     bool edge_fill = false;  // bounded: strips placed so that no lane is off the board (constructor)
@@ -346,7 +367,7 @@ struct StreamWave {
             const int64_t b0 = seg_begin;
             seg_begin = b0 + group_cut(len, role);
             seg_end = b0 + group_cut(len, role + 1);
-            if (!WRAP_ROWS) {
+            if (!WRAP_ROWS || kStage) {
                 // the group cut is float VALU math: without this the segment bounds live in 8 VGPRs, and
                 // the ghost-row variant spills at the 3-waves/SIMD budget (a scratch reload every loop
                 // trip; profiles/r1/ab_uniform.log: strip K = 12 86k -> 97k GCUPS); on a bounded board the
@@ -358,7 +379,7 @@ struct StreamWave {
             }
         }
         nsteps = (seg_end - seg_begin) + 2 * K;  // level-0 rows streamed
-        if (BOUNDED) seglen = (int)(seg_end - seg_begin);  // < 2^30 (plan_stream)
+        if (BOUNDED || kStage) seglen = (int)(seg_end - seg_begin);  // < 2^30 (plan_stream)
         ly0 = seg_begin - K;                     // level-0 row of step 0
         load_br = WRAP_ROWS ? floor_mod(ly0, a.rows) : ly0 + a.ghost;
         if (BOUNDED) {  // steps whose row lies on the board: global row a.y0 + ly0 + st in [0, height)
@@ -381,6 +402,12 @@ struct StreamWave {
             const int64_t cap = (int64_t)1 << 30;
             step_lo = (int)(lo < -cap ? -cap : (lo > cap ? cap : lo));
             step_hi = (int)(hi < -cap ? -cap : (hi > cap ? cap : hi));
+        }
+        if constexpr (kStage) {
+            const uint64_t pitch_bytes = (uint64_t)a.pitch * 4;
+            if (BOUNDED) lptr = (uint64_t)(uintptr_t)src + (uint64_t)load_br * pitch_bytes;  // (may precede the buffer)
+            sd = -R - 2 * K;  // the first store (at trip 0's top) is trip -1's: nothing valid
+            sptr = (uint64_t)(uintptr_t)dst + (uint64_t)((WRAP_ROWS ? 0 : a.ghost) + seg_begin + sd) * pitch_bytes;
         }
 #pragma unroll
         for (int g = 0; g < K; g++)
@@ -428,32 +455,38 @@ struct StreamWave {
         return (st >= mrow_lo && st < mrow_hi) ? 0xffffffffu : 0u;
     }
 
-    // kStage: prefetch the next R level-0 rows (steps first_step ..) into stage parity PAR (the row walk of load():
-    // wrap inside a single board, clamp to a ghost-row strip's buffer, clamp to a bounded board's buffer).
+    // kStage: prefetch the next R level-0 rows into stage parity PAR.  A bounded board walks a running address (two
+    // scalar adds per row instead of a clamp and a 64-bit multiply); its rows outside the buffer get an empty
+    // descriptor, so their loads return zeros that nothing uses unmasked.  The torus and ghost-row strips keep the
+    // row-index walk (wrap at the board's last row; clamp to the strip's buffer): the running address there measured
+    // 8 % slower on the (12, 2) torus with an instruction stream that differs only in scalar order
+    // (profiles/r3/ab_torus_load_addr.log, "new" vs "wl").
     template <int PAR>
-    __device__ __forceinline__ void stage_load(int64_t first_step) {
+    __device__ __forceinline__ void stage_load() {
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            int64_t br = load_br;
-            if (WRAP_ROWS) {
-                load_br = br + 1 == a.rows ? 0 : br + 1;
-            } else if (BOUNDED) {
-                int st = (int)first_step + r;
-                st = st < step_lo ? step_lo : (st > step_hi ? step_hi : st);
-                br = load_br + st;
+            __amdgpu_buffer_rsrc_t rs;
+            if constexpr (BOUNDED) {
+                const bool inside = lrow >= step_lo && lrow <= step_hi;
+                rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(lptr), (short)0, inside ? (int)span_bytes : 0,
+                                                       kRsrcWord3);
+                lptr += (uint64_t)a.pitch * 4;
+                lrow++;
             } else {
-                const int64_t buf_rows = a.rows + 2 * a.ghost;
-                load_br = br + 1;
-                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+                int64_t br = load_br;
+                if (WRAP_ROWS) {
+                    load_br = br + 1 == a.rows ? 0 : br + 1;
+                } else {
+                    const int64_t buf_rows = a.rows + 2 * a.ghost;
+                    load_br = br + 1;
+                    br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+                }
+                rs = row_rsrc(src + br * a.pitch, span_bytes);
             }
-            const __amdgpu_buffer_rsrc_t rs = row_rsrc(src + br * a.pitch, span_bytes);
 #pragma unroll
-            for (int j = 0; j < M; j++) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&(*stage)[PAR][0][r][j][0],
-                                                         4, load_off + 4 * j, 0, 0, 0);
-                if constexpr (kSeam)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&(*stage)[PAR][kSeam ? 1 : 0][r][j][0],
-                                                             4, seam_off + 4 * j, 0, 0, 0);
+            for (int d = 0; d < kDmas; d++) {
+                dma<kDmaWords>(rs, &(*stage)[PAR][0][r][d][0], load_off + 4 * d);
+                if constexpr (kSeam) dma<kDmaWords>(rs, &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
             }
         }
     }
@@ -463,12 +496,27 @@ struct StreamWave {
     struct Seam {
         uint32_t s[kSeam ? R : 1][M];
     };
+    // kStage: store the previous trip's R output rows (running store address; rows outside the segment -- the
+    // pipeline fill and the tail -- get an empty descriptor and are dropped)
+    __device__ __forceinline__ void store_staged(const uint32_t (&v)[R][M]) {
+        const uint64_t pitch_bytes = (uint64_t)a.pitch * 4;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int d = sd + r;
+            const bool valid = d >= 0 && d < seglen;
+            V::store(__builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sptr + r * pitch_bytes), (short)0,
+                                                       valid ? (int)span_bytes : 0, kRsrcWord3),
+                     store_off, v[r]);
+        }
+        sptr += R * pitch_bytes;
+        sd += R;
+    }
     template <int PAR>
     __device__ __forceinline__ void stage_read(uint32_t (&v)[R][M], int lane) {
 #pragma unroll
         for (int r = 0; r < R; r++)
 #pragma unroll
-            for (int j = 0; j < M; j++) v[r][j] = (*stage)[PAR][0][r][j][lane];
+            for (int j = 0; j < M; j++) v[r][j] = staged(PAR, 0, r, j, lane);
     }
     template <int PAR>
     __device__ __forceinline__ void stage_read_seam(Seam& t, int lane) {
@@ -476,7 +524,7 @@ struct StreamWave {
 #pragma unroll
             for (int r = 0; r < R; r++)
 #pragma unroll
-                for (int j = 0; j < M; j++) t.s[r][j] = (*stage)[PAR][kSeam ? 1 : 0][r][j][lane];
+                for (int j = 0; j < M; j++) t.s[r][j] = staged(PAR, kSeam ? 1 : 0, r, j, lane);
         }
     }
     // ... and make them the rows of steps first_step ..: kSeam, each word's high half from the seam word; bounded, rows
@@ -704,14 +752,14 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         uint32_t NV[R];  // (K = 1 neighbour words: unused here)
 #pragma unroll
         for (int r = 0; r < R; r++) NV[r] = 0;
-        w.template stage_load<0>(0);
+        w.template stage_load<0>();
         auto trip = [&](int64_t tt, auto skip, auto mask, auto par) {
             constexpr int PAR = decltype(par)::value;
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
-            w.store_masked(B, tt - 1);
+            w.store_staged(B);
             w.template stage_read<PAR>(B, lane);
             __builtin_amdgcn_sched_barrier(0);  // the row reads before the prefetch: their latency hides behind it
-            w.template stage_load<1 - PAR>((tt + 1) * R);
+            w.template stage_load<1 - PAR>();
             typename W::Seam st;
             w.template stage_read_seam<PAR>(st, lane);
             w.stage_in(B, st, tt * R);
@@ -754,7 +802,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             if (t < ntrips) trip(t++, NoSkip{}, Mask{}, P0{});
         }
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        w.store_masked(B, t - 1);
+        w.store_staged(B);
     } else if constexpr (!BOUNDED) {
         // K = 1 (rows of trip t in `cur`, trip t-1's outputs in `other`):
         //   [wait for all memory ops of trip t-1] [store `other`] [prefetch trip t+1 into `other`]
