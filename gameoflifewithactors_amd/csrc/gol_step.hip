@@ -188,7 +188,10 @@ struct StreamWave {
     // break produces spread one cell per generation: after K <= 16M generations they have not reached either
     // end of the seam lane, so lanes 0..62 are exact.  One halo lane per wave instead of two: a 65536-cell row
     // at M = 2 is 16 seam strips plus 16 blocks, against 17 strips of 62 (DESIGN.md 4.1 "Seam strips").
-    static constexpr bool kSeam = !BOUNDED && !(K == 1) && !kRagged;
+#ifndef GOL_AB_NOSEAM
+#define GOL_AB_NOSEAM 0
+#endif
+    static constexpr bool kSeam = !GOL_AB_NOSEAM && !BOUNDED && !(K == 1) && !kRagged;
     // Deep passes (K > 1) stage their prefetched rows through LDS (see `stage` below); the K = 1 pass keeps two
     // register buffers (it has registers to spare, and its halo-free strips load a neighbour word per row).
     static constexpr bool kStage = !kNoHalo;
@@ -959,12 +962,15 @@ int stream_pair_split(int k, int ilv, bool bounded) {
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
     // (12, 2) runs 12-wave workgroups at 3 waves/SIMD: three-way groups (profiles/r1/w12_sweep*.log)
-    // Bounded (16, 2) falls off a cliff above 0.6: 98.8k GCUPS at 0.6, 85.4k at 0.7, with the same
-    // instruction counts (profiles/r2/prio_split_j.log, split_bounded_i.log); the torus variants peak at 0.7.
+    // Round 3, staged passes, fresh 65536^2 board, forward + reverse sweep (profiles/r3/split_sweep_f.log): torus
+    // (12, 2) 0.64 / 0.68 / 0.72 -> 95.9k / 96.8k / 95.0k; torus (16, 2) 0.60 / 0.64 / 0.68 / 0.72 -> 101.8k / 107.5k /
+    // 107.6k / 104.7k; bounded (12, 2) 0.60 / 0.64 / 0.68 -> 96.6k / 99.0k / 95.4k; bounded (16, 2) 0.56 / 0.60 /
+    // 0.64 / 0.68 -> 112.5k / 112.0k / 106.2k / 100.7k (a slope now, not round 2's cliff).
     if (bounded && ilv == 2 && k == 16) return (int)(0.60 * 65536);
+    if (bounded && ilv == 2 && k == 12) return (int)(0.64 * 65536);
     if (ilv == 1 && k >= 24) return (int)(0.60 * 65536);
     if (ilv == 2 && k == 12) return (int)(0.70 * 65536);
-    if (ilv == 2 && k >= 16) return (int)(0.72 * 65536);
+    if (ilv == 2 && k >= 16) return (int)(0.66 * 65536);
     if (ilv == 4 && k >= 8) return (int)(0.55 * 65536);
     return 0;
 }
@@ -1004,7 +1010,7 @@ static int64_t seam_rem_units(const StreamArgs& a, int64_t nsegs, int64_t rem_mi
 // Does the seam geometry apply?  Torus deep passes (the bounded edge-fill strips keep their zero-fill edges) on rows
 // of at least one seam strip, with K <= 16 M (the break in the middle of the seam lane must not reach its ends).
 static bool seam_applies(const StreamArgs& a, int k, bool bounded) {
-    return a.seam_opt >= 0 && !bounded && !a.rag_bits && k > 1 && k <= 16 * a.ilv && a.words / a.ilv >= kSeamInterior;
+    return !GOL_AB_NOSEAM && a.seam_opt >= 0 && !bounded && !a.rag_bits && k > 1 && k <= 16 * a.ilv && a.words / a.ilv >= kSeamInterior;
 }
 
 // Work decomposition: nstrips column strips x nsegs row segments, one wave each (or one SIMD group of

@@ -22,6 +22,8 @@ def main():
     p.add_argument("--ilv", type=int, default=0, help="packed layout (0 = the engine default for the width)")
     p.add_argument("--split", type=float, default=None, help="board option 'split' (fraction; negative = off)")
     p.add_argument("--seam", type=int, default=0, help="board option 'seam' (0 = engine choice, -1 = halo-lane strips)")
+    p.add_argument("--pre", type=int, default=0, help="generations stepped before the timed passes (bench.py's window "
+                   "starts at generation 312)")
     a = p.parse_args()
     import torch
 
@@ -40,7 +42,7 @@ def main():
         with Board(W, H, a.boundary, tblock_k=k, ilv=ilv, options=opts) as b:
             b.seed_splitmix(0x5EED)
             s = torch.cuda.ExternalStream(b.stream)
-            b.step(2 * k)
+            b.step(2 * k + a.pre)
             b.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
@@ -49,7 +51,7 @@ def main():
             b.synchronize()
             t = e0.elapsed_time(e1) / 1e3 / a.passes
             gcups = W * H * k / t / 1e9
-            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
+            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "split": a.split, "pre": a.pre, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
                               "alg_GBps": round(W * H / 4 / t / 1e9, 1),
                               }), flush=True)
 
