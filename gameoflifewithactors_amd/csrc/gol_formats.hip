@@ -56,33 +56,59 @@ __global__ void gol_pack(const uint8_t* __restrict__ cells, uint32_t* __restrict
     words[(row0 + y) * pitch + w] = v;
 }
 
-// Ragged byte board (any width) -> whole consecutive words (the cooperative pass's scratch rows): one thread
-// per word of the `pitch`-word row, cells past W and words past ceil(W / 32) zero
-__global__ void gol_pack_ragged(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words, int64_t W, int64_t H,
-                                int64_t pitch) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= pitch * H) return;
-    const int64_t w = idx % pitch, y = idx / pitch;
-    const uint8_t* p = cells + y * W;
-    uint32_t v = 0;
-    for (int b = 0; b < 32; b++) {
-        const int64_t x = 32 * w + b;
-        if (x < W) v |= (uint32_t)(p[x] != 0) << b;
+// Ragged byte board (any width) <-> whole consecutive words (the scratch rows of the cooperative and streaming passes
+// on ragged boards: `pitch` words per row, bit b of word j = cell 32 j + b, cells past W and words past ceil(W / 32)
+// zero).  One wavefront per chunk of 64 words of one row (2048 cells): the bytes move as 64 consecutive cells per
+// wave instruction (coalesced byte loads / stores), the bits by ballot (pack) and readlane (unpack).  A thread per
+// word walking its own 32 bytes (the round-2 kernels) read the 65535^2 board at a small fraction of HBM rate.
+constexpr int kChunkWords = 64;
+
+__device__ __forceinline__ bool ragged_chunk(int64_t words_per_row, int64_t H, int64_t& y, int64_t& w0) {
+    const int64_t chunks = (words_per_row + kChunkWords - 1) / kChunkWords;
+    const int64_t u = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (u >= chunks * H) return false;
+    y = u / chunks;
+    w0 = (u - y * chunks) * kChunkWords;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void gol_pack_ragged(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words,
+                                                        int64_t W, int64_t H, int64_t pitch) {
+    int64_t y, w0;
+    if (!ragged_chunk(pitch, H, y, w0)) return;
+    const int lane = threadIdx.x & 63;
+    // the row as a buffer resource: cells past W read as 0 (range check), so the loads carry no branch and all 32 are
+    // in flight at once
+    const __amdgpu_buffer_rsrc_t row =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cells + y * W), (short)0, (int)W, 0x00020000);
+    uint8_t v[kChunkWords / 2];
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b8(row, (int)((w0 + 2 * i) * 32) + lane, 0, 0);
+    uint32_t mine = 0;  // word w0 + lane
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++) {
+        const uint64_t m = __ballot(v[i] != 0);
+        mine = lane == 2 * i ? (uint32_t)m : (lane == 2 * i + 1 ? (uint32_t)(m >> 32) : mine);
     }
-    words[idx] = v;
+    if (w0 + lane < pitch) words[y * pitch + w0 + lane] = mine;
 }
 // ... and back: the W cells of each row as 0 / 1 bytes (the byte board's own values)
-__global__ void gol_unpack_ragged(const uint32_t* __restrict__ words, uint8_t* __restrict__ cells, int64_t W, int64_t H,
-                                  int64_t pitch) {
+__global__ __launch_bounds__(256) void gol_unpack_ragged(const uint32_t* __restrict__ words, uint8_t* __restrict__ cells,
+                                                          int64_t W, int64_t H, int64_t pitch) {
     const int64_t nw = (W + 31) / 32;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= nw * H) return;
-    const int64_t w = idx % nw, y = idx / nw;
-    const uint32_t v = words[y * pitch + w];
-    uint8_t* p = cells + y * W;
-    for (int b = 0; b < 32; b++) {
-        const int64_t x = 32 * w + b;
-        if (x < W) p[x] = (uint8_t)((v >> b) & 1u);
+    int64_t y, w0;
+    if (!ragged_chunk(nw, H, y, w0)) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t mine = w0 + lane < nw ? words[y * pitch + w0 + lane] : 0u;
+    // stores past the row's W cells are dropped by the buffer range check
+    const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(cells + y * W, (short)0, (int)W, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * i);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * i + 1);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(((lane < 32 ? lo : hi) >> (lane & 31)) & 1u), row,
+                                             (int)((w0 + 2 * i) * 32) + lane, 0, 0);
     }
 }
 
@@ -321,14 +347,23 @@ hipError_t launch_pack(const uint8_t* cells, uint32_t* words, int64_t W, int64_t
     return hipGetLastError();
 }
 
+// one wave (of 4 per 256-thread block) per 64-word chunk of a row
+static unsigned ragged_blocks(int64_t words_per_row, int64_t H) {
+    return (unsigned)(((words_per_row + kChunkWords - 1) / kChunkWords * H + 3) / 4);
+}
+
 hipError_t launch_pack_ragged(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int64_t pitch, hipStream_t s) {
-    hipLaunchKernelGGL(gol_pack_ragged, dim3(grid1d(pitch * H)), dim3(256), 0, s, cells, words, W, H, pitch);
+    // rows are addressed through 32-bit buffer offsets
+    if (pitch < (W + 31) / 32 || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gol_pack_ragged, dim3(ragged_blocks(pitch, H)), dim3(256), 0, s, cells, words, W, H, pitch);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int64_t pitch,
                                 hipStream_t s) {
-    hipLaunchKernelGGL(gol_unpack_ragged, dim3(grid1d((W + 31) / 32 * H)), dim3(256), 0, s, words, cells, W, H, pitch);
+    if (pitch < (W + 31) / 32 || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gol_unpack_ragged, dim3(ragged_blocks((W + 31) / 32, H)), dim3(256), 0, s, words, cells, W, H,
+                       pitch);
     return hipGetLastError();
 }
 

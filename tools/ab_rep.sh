@@ -8,7 +8,7 @@ for rep in $(seq $reps); do
     for cfg in $cfgs; do
       ilv=${cfg%%:*}; ks=${cfg#*:}
       echo "rep=$rep lib=$(basename $L) ilv=$ilv" >> $out
-      GOL_LIB=$PWD/$L timeout -k 10 120 python tools/sweep.py --ilv $ilv --ks $ks --passes 16 --boundary ${AB_BOUNDARY:-0} 2>/dev/null | grep '^{' >> $out || exit 1
+      GOL_LIB=$PWD/$L timeout -k 10 120 python tools/sweep.py --ilv $ilv --ks $ks --passes 16 --boundary ${AB_BOUNDARY:-0} --pre ${AB_PRE:-0} 2>/dev/null | grep '^{' >> $out || exit 1
     done
   done
 done
