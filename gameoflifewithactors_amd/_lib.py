@@ -124,10 +124,29 @@ SIGNATURES = {
 }
 
 
-def device_code_fingerprint(path: str = LIB_PATH) -> str | None:
-    """sha256 (first 16 hex digits) of the gfx950 device code in a built library: the ELF section `.hip_fatbin`,
-    which holds every kernel's code object.  PMC measurements (profiles/pmc_traffic.json) record it, and bench.py
-    uses a measurement only for the build it was taken on."""
+def _elf_sections(data: bytes, base: int = 0):
+    """(name, offset, size) of every section of the 64-bit little-endian ELF image at data[base:]."""
+    import struct
+
+    shoff, = struct.unpack_from("<Q", data, base + 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, base + 0x3A)
+
+    def sec(i):
+        name, _type, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, base + shoff + i * shentsize)
+        return name, off, size
+
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", base + stroff + name)
+        yield data[base + stroff + name:end].decode(errors="replace"), off, size
+
+
+def device_code_fingerprint(path: str = LIB_PATH, kernel: str = "gol_stream_step") -> str | None:
+    """sha256 (first 16 hex digits) of the gfx950 code object that holds `kernel` (the translation unit of the hot
+    kernel, csrc/gol_step.hip) inside a built library's `.hip_fatbin`.  PMC measurements (profiles/pmc_traffic.json)
+    record it, and bench.py uses a measurement only for the device code it was taken on; edits to the other
+    translation units (formats, coop, ...) leave it unchanged."""
     import hashlib
     import struct
 
@@ -138,20 +157,27 @@ def device_code_fingerprint(path: str = LIB_PATH) -> str | None:
         return None
     if data[:4] != b"\x7fELF" or data[4] != 2:
         return None
-    shoff, = struct.unpack_from("<Q", data, 0x28)
-    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
-
-    def sec(i):
-        name, _type, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
-        return name, off, size
-
-    _, stroff, _ = sec(shstrndx)
-    for i in range(shnum):
-        name, off, size = sec(i)
-        end = data.index(b"\0", stroff + name)
-        if data[stroff + name:end] == b".hip_fatbin":
-            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
-    return None
+    fat = next(((off, size) for name, off, size in _elf_sections(data) if name == ".hip_fatbin"), None)
+    if fat is None:
+        return None
+    blob = data[fat[0]:fat[0] + fat[1]]
+    # the device code objects are whole ELF images inside the offload bundles: hash the one(s) naming the kernel
+    h = hashlib.sha256()
+    found = False
+    pos = blob.find(b"\x7fELF")
+    while pos >= 0:
+        try:
+            shoff, = struct.unpack_from("<Q", blob, pos + 0x28)
+            shentsize, shnum = struct.unpack_from("<HH", blob, pos + 0x3A)
+            size = shoff + shentsize * shnum
+        except struct.error:
+            break
+        image = blob[pos:pos + size]
+        if kernel.encode() in image:
+            h.update(image)
+            found = True
+        pos = blob.find(b"\x7fELF", pos + max(size, 4))
+    return h.hexdigest()[:16] if found else None
 
 
 def hip_runtimes() -> list:
