@@ -12,7 +12,7 @@ G[1]="FETCH_SIZE"
 G[2]="WRITE_SIZE"
 G[3]="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 G[4]="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
-G[5]="TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum"
+G[5]="TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum"  # at most 4 TCC counters per pass
 for i in $groups; do
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$i]} --output-format csv -d $out/g$i -o run -- $cmd > $out/g$i.log 2>&1 || { echo "group $i failed rc=$?"; tail -3 $out/g$i.log; }
 done

@@ -36,6 +36,9 @@ __global__ __launch_bounds__(256) void NAME(uint32_t* out, uint32_t seed) {     
 #define I_ALIGN(r) asm volatile("v_alignbit_b32 %0, %1, %0, 31" : "+v"(r) : "v"(b));
 #define I_BFI(r) asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(r) : "v"(b), "v"(c));
 #define I_DPP(r) asm volatile("v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(r));
+#define I_DPPROR(r) asm volatile("v_mov_b32_dpp %0, %0 wave_ror:1 row_mask:0xf bank_mask:0xf" : "+v"(r));
+#define I_DPPROL(r) asm volatile("v_mov_b32_dpp %0, %0 wave_rol:1 row_mask:0xf bank_mask:0xf" : "+v"(r));
+#define I_DPPSHL(r) asm volatile("v_mov_b32_dpp %0, %0 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(r));
 #define I_DPPROW(r) asm volatile("v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(r));
 #define I_XORDPP(r) asm volatile("v_xor_b32_dpp %0, %1, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(r) : "v"(b));
 #define I_LSHL(r) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(r));
@@ -67,6 +70,9 @@ DEF_KERNEL(k_align, I_ALIGN)
 DEF_KERNEL(k_bfi, I_BFI)
 DEF_KERNEL(k_dpp, I_DPP)
 DEF_KERNEL(k_dpprow, I_DPPROW)
+DEF_KERNEL(k_dppror, I_DPPROR)
+DEF_KERNEL(k_dpprol, I_DPPROL)
+DEF_KERNEL(k_dppshl, I_DPPSHL)
 DEF_KERNEL(k_xordpp, I_XORDPP)
 DEF_KERNEL(k_lshl, I_LSHL)
 DEF_KERNEL(k_andor, I_ANDOR)
@@ -98,6 +104,7 @@ int main() {
     struct { const char* name; kfn f; } ks[] = {
         {"v_xor_b32", k_xor}, {"v_bitop3_b32", k_bitop3}, {"v_alignbit_b32", k_align},
         {"v_bfi_b32", k_bfi}, {"v_mov_b32_dpp wave_shr", k_dpp}, {"v_mov_b32_dpp row_shr", k_dpprow},
+        {"v_mov_b32_dpp wave_ror", k_dppror}, {"v_mov_b32_dpp wave_rol", k_dpprol}, {"v_mov_b32_dpp wave_shl", k_dppshl},
         {"v_xor_b32_dpp row_shr", k_xordpp}, {"v_lshlrev_b32", k_lshl}, {"v_and_or_b32", k_andor},
         {"v_lshl_or_b32", k_lshlor}, {"v_lshlrev_b64", k_lshl64}, {"v_lshrrev_b64", k_lshr64},
         {"v_lshl_add_u64", k_lshladd64}, {"v_add_u32", k_add}, {"v_addc_co_u32", k_addc}, {"v_or_b32", k_or},
