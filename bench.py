@@ -41,10 +41,9 @@ def default_depth(lib, ilv: int, world: int, boundary: str) -> int:
     kernel.  Torus, single board or ghost-row strips (N > 1): the engine default K = 12 at M = 2 (12-wave
     workgroups).  Over the whole 10k-generation job it beats K = 16 on both: single board 116.4k vs 109.5k
     GCUPS (profiles/r1/bench_k_ab.log), strips 113.7-114.1k vs 99.2-101.0k (strip_k_ab.log); K = 16 wins only
-    on the first passes of a fresh board (ghost_ab2.log).  Bounded boards at M = 2 keep 8-wave workgroups,
-    where K = 16 is faster (78.5k vs 74.2k, profiles/r1/strip_bounded_sweep_wpb.log)."""
-    if ilv == 2 and boundary == "bounded":
-        return 16
+    on the first passes of a fresh board (ghost_ab2.log).  Bounded boards too since round 3's staged passes:
+    127.5k vs 119.2k GCUPS over the whole job (profiles/r3/bench_bounded_job_d.log)."""
+    del boundary
     return int(lib.gol_default_tblock(ilv))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")

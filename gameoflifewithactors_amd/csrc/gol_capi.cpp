@@ -190,10 +190,12 @@ int board_tblock(int ilv, int64_t cells, int boundary) {
     // byte boards (ragged widths): the ragged streaming pass runs ilv 1 words, as small ilv-1 boards do
     if (ilv == 0) return cells < kSmallBoardCells ? 8 : 16;
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
-    // bounded boards: the masked variant runs best one level deeper (profiles/r1/strip_bounded_sweep.log).
-    // Ghost-row strips (multi-GPU) keep K = 12: over a whole 10k-generation job 114k vs 100k GCUPS for
-    // K = 16 (profiles/r1/strip_k_ab.log), although K = 16 leads on a fresh board's first passes.
-    if (ilv == 2 && (boundary == GOL_BOUNDED || cells < kMidBoardCells)) return 16;
+    // Mid-size boards run one level deeper.  Large bounded boards ran best at K = 16 in rounds 1-2 (the masked
+    // variant); since round 3's staged passes K = 12 leads there as on the torus: the whole 10k-generation job at
+    // 65536^2 127.5k vs 119.2k GCUPS (profiles/r3/bench_bounded_job_d.log).  Ghost-row strips (multi-GPU) keep
+    // K = 12: over a whole job 114k vs 100k GCUPS for K = 16 (profiles/r1/strip_k_ab.log).
+    (void)boundary;
+    if (ilv == 2 && cells < kMidBoardCells) return 16;
     return default_tblock(ilv);
 }
 
