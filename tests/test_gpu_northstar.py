@@ -70,10 +70,19 @@ def test_single_board_shipped_defaults(gol, name):
     c = _case(name)
     with gol.Board(c["width"], c["height"], c["boundary"]) as b:
         info = b.info()
-        assert info["ilv"] == 2 and info["tblock_k"] == (12 if c["boundary"] == gol.TORUS else 16)
+        assert info["ilv"] == 2 and info["tblock_k"] == 12  # both boundaries since round 3
         b.seed_splitmix(c["seed"])
         _walk(b, c, b.step, lambda: (b.hash(), b.population()))
         assert b.generation == c["generations"]
+
+
+def test_single_board_bounded_k16(gol):
+    """The bounded board at K = 16 (its default before round 3, still the depth of mid-size boards)."""
+    c = _case("n1_65536_bounded")
+    with gol.Board(c["width"], c["height"], c["boundary"], tblock_k=16) as b:
+        assert b.info()["tblock_k"] == 16
+        b.seed_splitmix(c["seed"])
+        _walk(b, c, b.step, lambda: (b.hash(), b.population()))
 
 
 @pytest.mark.parametrize("name", ["n1_65536_torus", "c4_262144_torus"])
