@@ -69,6 +69,17 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);              // wave_shl:1
 }
 
+// Prefetch placement of the deep passes on seam strips (torus), GOL_SEAM_SPREAD: 0 = all R rows' DMAs at the trip's
+// top (the bounded passes' placement), 1 = one row's DMAs after each of the first R generation levels, 3 = the rows'
+// own-word DMAs at the top and one row's seam DMAs after each of the first R levels, 4 = row r's own-word DMAs after
+// level 2r and its seam DMAs after level 2r + 1; -1 (default) = 4 at K >= 16, else 1.  Rows a short pass (K below the
+// levels a mode needs) has not issued by its last level are issued after it; the pipeline-fill trips (which skip
+// levels) keep every DMA at the top.  Round 3, interleaved on one box at generation 300 (profiles/r3/ab_spread_modes_i.log),
+// GCUPS for modes 1 / 0 / 3 / 4: (12, 2) 114.3 / 113.4 / 113.6 / 113.8, (16, 2) 115.2 / 113.0 / 115.4 / 116.5.
+// On bounded boards (no seam DMAs) spreading lost 5 % (profiles/r3/ab_spread_h.log): they keep mode 0.
+#ifndef GOL_SEAM_SPREAD
+#define GOL_SEAM_SPREAD -1
+#endif
 // GOL_STAMP (diagnostic builds only): every wave records its start / end time (s_memrealtime, 100 MHz)
 // into g_stamps; gol_debug_stamps() copies them out (tools/tail.py measures the launch tail)
 #ifndef GOL_STAMP
@@ -467,7 +478,18 @@ struct StreamWave {
     template <int PAR>
     __device__ __forceinline__ void stage_load() {
 #pragma unroll
-        for (int r = 0; r < R; r++) {
+        for (int r = 0; r < R; r++) stage_load_row<PAR, 3>(r);
+    }
+    // KINDS: 1 = the row's own-word DMAs (advancing the row walk; the descriptor is kept for the seam DMAs), 2 = its
+    // seam DMAs (kept descriptor), 3 = both
+    __amdgpu_buffer_rsrc_t row_rs[R];
+    template <int PAR, int KINDS>
+    __device__ __forceinline__ void stage_load_row(int r) {
+        if constexpr ((KINDS & 1) == 0) {
+#pragma unroll
+            for (int d = 0; d < kDmas; d++)
+                if constexpr (kSeam) dma<kDmaWords>(row_rs[r], &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
+        } else {
             __amdgpu_buffer_rsrc_t rs;
             if constexpr (BOUNDED) {
                 const bool inside = lrow >= step_lo && lrow <= step_hi;
@@ -486,10 +508,11 @@ struct StreamWave {
                 }
                 rs = row_rsrc(src + br * a.pitch, span_bytes);
             }
+            if constexpr ((KINDS & 2) == 0) row_rs[r] = rs;
 #pragma unroll
             for (int d = 0; d < kDmas; d++) {
                 dma<kDmaWords>(rs, &(*stage)[PAR][0][r][d][0], load_off + 4 * d);
-                if constexpr (kSeam) dma<kDmaWords>(rs, &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
+                if constexpr (kSeam && (KINDS & 2)) dma<kDmaWords>(rs, &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
             }
         }
     }
@@ -577,8 +600,8 @@ struct StreamWave {
 
     // Push R rows (steps t*R .. t*R+R-1) through the K levels; v[r] becomes row (ly0 + t*R + r - K) of
     // generation K.  SKIP: leave out levels whose inputs in this trip are all pipeline fill (garbage).
-    template <bool SKIP, bool MASK>
-    __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
+    template <bool SKIP, bool MASK, typename Hook>
+    __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t, Hook&& hook) {
         [[maybe_unused]] const int64_t lyt = ly0 + t * R;
         if constexpr (kNoHalo) {  // K = 1: lanes 0 / 63 keep the loaded neighbour word (bound_ctrl off)
 #pragma unroll
@@ -615,7 +638,7 @@ struct StreamWave {
         for (int r = 0; r < R; r++) right[r] = from_right<!BOUNDED>(v[r][0]);
 #pragma unroll
         for (int g = 0; g < K; g++) {
-            if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on
+            if (SKIP && t * R + R - 1 < 2 * g) continue;  // level g's inputs are valid from step 2g on (SKIP: no hook)
 #pragma unroll
             for (int r = 0; r < R; r += 2) {
                 uint32_t m0 = 0xffffffffu, m1 = 0xffffffffu;
@@ -641,7 +664,12 @@ struct StreamWave {
                 }
             }
             __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges
+            hook(g);
         }
+    }
+    template <bool SKIP, bool MASK>
+    __device__ __forceinline__ void process(uint32_t (&v)[R][M], const uint32_t (&nb)[R], int64_t t) {
+        process<SKIP, MASK>(v, nb, t, [](int) {});
     }
 
     __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
@@ -762,12 +790,49 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             w.store_staged(B);
             w.template stage_read<PAR>(B, lane);
             __builtin_amdgcn_sched_barrier(0);  // the row reads before the prefetch: their latency hides behind it
-            w.template stage_load<1 - PAR>();
+            // prefetch placement (GOL_SEAM_SPREAD above): rows issued at the top, after level g, and after the levels
+            // (the pipeline-fill trips, which skip levels, keep every DMA at the top)
+            constexpr int kSpread = GOL_SEAM_SPREAD >= 0 ? GOL_SEAM_SPREAD : (K >= 16 ? 4 : 1);
+            constexpr int kMode = W::kSeam && !decltype(skip)::value ? kSpread : 0;
+            if constexpr (kMode == 0) w.template stage_load<1 - PAR>();
+            if constexpr (kMode == 3) {
+#pragma unroll
+                for (int r = 0; r < R; r++) w.template stage_load_row<1 - PAR, 1>(r);
+            }
             typename W::Seam st;
             w.template stage_read_seam<PAR>(st, lane);
             w.stage_in(B, st, tt * R);
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
-            w.template process<decltype(skip)::value, decltype(mask)::value>(B, NV, tt);
+            auto hook = [&](int g) {
+                if constexpr (kMode == 1 || kMode == 3) {
+                    if (g < R) {
+                        w.template stage_load_row<1 - PAR, kMode == 1 ? 3 : 2>(g);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else if constexpr (kMode == 4) {
+                    if (g < 2 * R) {
+                        if (g % 2 == 0)
+                            w.template stage_load_row<1 - PAR, 1>(g / 2);
+                        else
+                            w.template stage_load_row<1 - PAR, 2>(g / 2);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            };
+            w.template process<decltype(skip)::value, decltype(mask)::value>(B, NV, tt, hook);
+            // a pass shallower than the levels the mode spreads over: the rows not yet issued
+            if constexpr (kMode == 1 || kMode == 3) {
+#pragma unroll
+                for (int r = K; r < R; r++) w.template stage_load_row<1 - PAR, kMode == 1 ? 3 : 2>(r);
+            } else if constexpr (kMode == 4) {
+#pragma unroll
+                for (int g = K; g < 2 * R; g++) {
+                    if (g % 2 == 0)
+                        w.template stage_load_row<1 - PAR, 1>(g / 2);
+                    else
+                        w.template stage_load_row<1 - PAR, 2>(g / 2);
+                }
+            }
         };
         using Mask = std::true_type;
         using NoMask = std::false_type;
