@@ -187,8 +187,11 @@ int board_ilv(int64_t width, int64_t height, int nparts) {
 }
 
 int board_tblock(int ilv, int64_t cells, int boundary) {
-    // byte boards (ragged widths): the ragged streaming pass runs ilv 1 words, as small ilv-1 boards do
-    if (ilv == 0) return cells < kSmallBoardCells ? 8 : 16;
+    // byte boards (ragged widths): the ragged streaming pass runs ilv 1 words, as small ilv-1 boards do; one level
+    // deeper above 2^27 cells (torus, per generation, K = 16 / 24: 10001^2 3.6-3.8 / 4.4-4.6 us, 16383^2 7.7-8.2 /
+    // 7.0-7.2, 23171^2 12.5-12.9 / 12.0-12.3, 32767^2 23.2-23.5 / 22.3-22.4, 65535^2 84.4-85.6 / 83.7-84.1;
+    // profiles/r3/ragged_stream_k_b.log, ragged_stream_k_m.log)
+    if (ilv == 0) return cells < kSmallBoardCells ? 8 : (cells < ((int64_t)1 << 27) ? 16 : 24);
     if (ilv == 1 && cells < kSmallBoardCells) return 8;
     // Mid-size boards run one level deeper.  Large bounded boards ran best at K = 16 in rounds 1-2 (the masked
     // variant); since round 3's staged passes K = 12 leads there as on the torus: the whole 10k-generation job at
@@ -245,6 +248,12 @@ struct gol_board {
     unsigned coop_epoch = 0;            // tag epoch of the last cooperative launch (1..65535)
     uint32_t* rag[2] = {nullptr, nullptr};  // ragged byte boards on the cooperative pass: whole-word scratch rows
     int64_t rag_words = 0;                  // capacity of each rag buffer
+    // Ragged byte boards between gol_step calls of the multi-generation passes keep their state in the scratch rows:
+    // 0 = the bytes (cells(cur)) are current; 1 = rag[rag_cur] holds it in the streaming pass's rows (rag_pitch words),
+    // 2 = in the cooperative pass's rows.  Every other access first brings the bytes up to date (sync_bytes).
+    int rag_state = 0;
+    int rag_cur = 0;
+    int64_t rag_pitch = 0;
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -306,10 +315,21 @@ int sync(gol_board* b) {
     return check_valid(b);
 }
 
-// The board's cells were replaced as a whole: a timed-out hand-off no longer matters.
+// The board's cells were replaced as a whole: a timed-out hand-off no longer matters, and a ragged board's scratch
+// rows no longer hold its state.
 int overwritten(gol_board* b) {
     b->invalid = false;
+    b->rag_state = 0;
     return sync(b);
+}
+
+// A ragged byte board whose state the multi-generation passes left in the scratch rows (rag_state): unpack it into
+// the bytes, on the board's stream, before anything reads or modifies them.
+int sync_bytes(gol_board* b) {
+    if (!b->rag_state) return GOL_OK;
+    GOL_HIP(gol::launch_unpack_ragged(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_pitch, b->stream));
+    b->rag_state = 0;
+    return GOL_OK;
 }
 
 int set_cells_impl(gol_board* b, const uint8_t* host) {
@@ -337,6 +357,7 @@ int set_cells_impl(gol_board* b, const uint8_t* host) {
 
 int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
     if (b->multi) return b->multi->readback(host, stride, value);
+    if (int rc = sync_bytes(b)) return rc;
     const size_t n = (size_t)(stride * b->H);
     uint8_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, n);
@@ -364,6 +385,7 @@ int readback_impl(gol_board* b, uint8_t* host, int64_t stride, uint8_t value) {
 
 int reduce_impl(gol_board* b, bool hash, uint64_t* out) {
     if (b->multi) return b->multi->reduce(hash, out);
+    if (int rc = sync_bytes(b)) return rc;
     GOL_HIP(hipMemsetAsync(b->acc, 0, sizeof(unsigned long long), b->stream));
     if (b->packed) {
         if (hash)
@@ -511,7 +533,18 @@ bool use_stream_ragged(const gol_board* b) {
 
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
-    if (gens > 0 && use_wave_resident(b)) {
+    if (gens <= 0) return GOL_OK;
+    // the pass this call takes on a ragged byte board: 2 = cooperative, 1 = streaming (both on whole-word scratch rows
+    // that keep the state after the call), 0 = a byte pass (the bytes must be current)
+    int64_t rag_pitch = 0;
+    const bool wave = use_wave_resident(b);
+    const int rag_next = wave ? 0
+                              : (gens >= kCoopRaggedMinGens && use_coop_ragged(b, &rag_pitch)
+                                     ? 2
+                                     : (gens >= kStreamRaggedMinGens && use_stream_ragged(b) ? 1 : 0));
+    if (b->rag_state != rag_next)
+        if (int rc = sync_bytes(b)) return rc;
+    if (wave) {
         while (gens > 0) {
             const int64_t g = gens < kResidentMaxGensPerLaunch ? gens : kResidentMaxGensPerLaunch;
             GOL_HIP(gol::launch_wave_resident(b->buf[b->cur], b->buf[b->cur ^ 1], b->W, b->H, b->pitch, g,
@@ -522,27 +555,34 @@ int step_impl(gol_board* b, int64_t gens) {
         }
         return GOL_OK;
     }
-    if (gens > 0 && use_coop(b)) {
+    if (use_coop(b)) {
         uint32_t* bufs[2] = {b->words(0), b->words(1)};
         return coop_steps(b, b->W, b->pitch, b->ilv, 0, bufs, &b->cur, gens);
     }
-    int64_t rag_pitch = 0;
-    if (gens >= kCoopRaggedMinGens && use_coop_ragged(b, &rag_pitch)) {
-        // the ragged byte board as whole words in scratch rows, the pass, and back to bytes
-        if (int rc = ensure_rag(b, rag_pitch * b->H)) return rc;
-        GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, rag_pitch, b->stream));
-        int rc_cur = 0;
-        if (int rc = coop_steps(b, rag_pitch * 32, rag_pitch, 1, b->W, b->rag, &rc_cur, gens)) return rc;
-        GOL_HIP(gol::launch_unpack_ragged(b->rag[rc_cur], b->cells(b->cur ^ 1), b->W, b->H, rag_pitch, b->stream));
-        b->cur ^= 1;
-        return GOL_OK;
+    if (rag_next == 2) {
+        // the ragged byte board as whole words in scratch rows (packed once, kept there after the call), the pass
+        if (b->rag_state != 2) {
+            if (int rc = ensure_rag(b, rag_pitch * b->H)) return rc;
+            GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, rag_pitch, b->stream));
+            b->rag_cur = 0;
+        }
+        int rc_cur = b->rag_cur;
+        const int rc = coop_steps(b, rag_pitch * 32, rag_pitch, 1, b->W, b->rag, &rc_cur, gens);
+        b->rag_state = 2;
+        b->rag_cur = rc_cur;
+        b->rag_pitch = rag_pitch;
+        return rc;
     }
-    if (gens >= kStreamRaggedMinGens && use_stream_ragged(b)) {
-        // the ragged byte board as whole words in scratch rows, streaming passes, and back to bytes
+    if (rag_next == 1) {
+        // the ragged byte board as whole words in scratch rows (packed once, kept there after the call), streaming
         const int64_t nw = (b->W + 31) / 32;
-        if (int rc = ensure_rag(b, nw * b->H)) return rc;
-        GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, nw, b->stream));
-        int rc_cur = 0;
+        if (b->rag_state != 1) {
+            if (int rc = ensure_rag(b, nw * b->H)) return rc;
+            GOL_HIP(gol::launch_pack_ragged(b->cells(b->cur), b->rag[0], b->W, b->H, nw, b->stream));
+            b->rag_cur = 0;
+        }
+        b->rag_state = 1;
+        b->rag_pitch = nw;
         while (gens > 0) {
             const int k = gol::stream_largest_k(gens, b->tblock, 1);
             gol::StreamArgs a = b->stream_args(0, b->H, k);
@@ -550,17 +590,15 @@ int step_impl(gol_board* b, int64_t gens) {
             a.pitch = nw;
             a.ilv = 1;
             a.rag_bits = (int32_t)(b->W % 32);
-            GOL_HIP(gol::launch_stream_step(b->rag[rc_cur], b->rag[rc_cur ^ 1], a, k, b->boundary == GOL_BOUNDED,
+            GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, b->boundary == GOL_BOUNDED,
                                             b->boundary == GOL_TORUS, b->stream));
-            rc_cur ^= 1;
+            b->rag_cur ^= 1;
             b->generation += k;
             gens -= k;
         }
-        GOL_HIP(gol::launch_unpack_ragged(b->rag[rc_cur], b->cells(b->cur ^ 1), b->W, b->H, nw, b->stream));
-        b->cur ^= 1;
         return GOL_OK;
     }
-    if (gens > 0 && b->W * b->H <= resident_max_cells(b) &&
+    if (b->W * b->H <= resident_max_cells(b) &&
         (b->packed ? b->ilv == 1 && gol::resident_packed_fits(b->W, b->H) : gol::resident_bytes_fits(b->W, b->H))) {
         const bool bounded = b->boundary == GOL_BOUNDED;
         while (gens > 0) {
@@ -604,6 +642,7 @@ int place_points(gol_board* b, const std::vector<int64_t>& xy) {
     const int64_t n = (int64_t)xy.size() / 2;
     if (n == 0) return GOL_OK;
     if (b->multi) return b->multi->place_points(xy);
+    if (int rc = sync_bytes(b)) return rc;
     int64_t* d = nullptr;
     hipError_t e = hipMalloc(&d, xy.size() * sizeof(int64_t));
     if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc points");
@@ -903,6 +942,7 @@ int gol_get_region(gol_board* b, int64_t x, int64_t y, int64_t w, int64_t h, uin
         return fail(GOL_ERR_INVALID, "region outside the board");
     if (w == 0 || h == 0) return GOL_OK;
     if (b->multi) return b->multi->region(x, y, w, h, out);
+    if (int rc = sync_bytes(b)) return rc;
     uint8_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, (size_t)(w * h));
     if (e != hipSuccess) return fail(GOL_ERR_OOM, "hipMalloc region");
@@ -933,6 +973,7 @@ int gol_save_packed(gol_board* b, uint64_t* words, int64_t len) {
     const int64_t nc = (b->W + 63) / 64;
     if (!words || len != nc * b->H) return fail(GOL_ERR_INVALID, "words length must be height * ceil(width/64)");
     if (b->multi) return b->multi->save_packed(words);
+    if (int rc = sync_bytes(b)) return rc;
     const size_t n = (size_t)len * 8;
     uint64_t* staging = nullptr;
     hipError_t e = hipMalloc(&staging, n);
