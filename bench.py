@@ -96,7 +96,7 @@ def parse():
                    "several ranks share one GPU in rehearsals)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--handle-leg-child", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--handle-timeout", type=float, default=300.0,
+    p.add_argument("--handle-timeout", type=float, default=180.0,
                    help="seconds the one-process handle leg (a child process of rank 0) may take")
     p.add_argument("--handle-parts", type=int, default=-1,
                    help="one-process C-ABI leg (gol_create_multi, csrc/gol_multi.cpp: what the F# drop-in calls): "
