@@ -20,6 +20,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--size", type=int, default=65536)
     p.add_argument("--k", type=int, default=16)
+    p.add_argument("--boundary", type=int, default=0)
+    p.add_argument("--pre", type=int, default=0, help="generations stepped before the stamped passes")
     a = p.parse_args()
     from gameoflifewithactors_amd import Board, _lib
 
@@ -27,8 +29,10 @@ def main():
     fn = lib.gol_debug_stamps
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_longlong]
     n = a.size
-    with Board(n, n, tblock_k=a.k) as b:
+    with Board(n, n, a.boundary, tblock_k=a.k) as b:
         b.seed_splitmix(1)
+        if a.pre:
+            b.step(a.pre)
         for rep in range(3):
             b.step(a.k)
             b.synchronize()
@@ -49,7 +53,7 @@ def main():
                               "end_p90_us": round(float(np.percentile(ends, 90)), 1),
                               "util": round(busy.sum() / (span * m.sum()), 4)}), flush=True)
             if rep == 0:
-                np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{n}_k{a.k}.npy"), buf)
+                np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{n}_k{a.k}_b{a.boundary}.npy"), buf)
             buf[:] = 0
 
 
