@@ -1,4 +1,4 @@
-# GPU call script (gpurun): each step under its own time limit, chained so that a failure ends the call
+# GPU call script (gpurun): the current measurement call; each step under its own time limit, chained so that a failure ends the call
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r3r; mkdir -p $O
