@@ -105,7 +105,9 @@ int gol_clear(gol_board* b);
  * phase barrier).  Asynchronous with respect to the host; any readback synchronises (and reports a failed
  * cooperative pass: the board is then invalid until overwritten).  Small and mid-size boards run the whole call
  * as one launch (single-wave, cooperative or LDS-resident pass: DESIGN.md 4.3-4.5; gol_set_option moves the
- * cut-overs); results are identical either way. */
+ * cut-overs); results are identical either way.  A board whose width is not a multiple of 32 runs calls of several
+ * generations on whole-word scratch rows (DESIGN.md 4.1 "Ragged rows") and keeps its state there until another
+ * call reads or replaces the cells. */
 int gol_step(gol_board* b, int64_t generations);
 int gol_generation(gol_board* b, int64_t* out);
 int gol_synchronize(gol_board* b);
@@ -151,6 +153,8 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *                                (0: the measured default, -1: no split)
  *   "seg_rows" 0 | n             streaming pass: rows per wave segment (0: planned)
  *   "seam" 0 | -1                streaming pass on a torus: seam strips where they apply (-1: halo-lane strips)
+ *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
+ *                                words (0: the per-generation byte step)
  *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments
  *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
  *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)
