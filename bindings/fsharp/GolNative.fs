@@ -36,6 +36,12 @@ extern int gol_population(nativeint board, int64& out)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gol_hash(nativeint board, uint64& out)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_synchronize(nativeint board)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_set_option(nativeint board, [<MarshalAs(UnmanagedType.LPStr)>] string name, int64 value)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_transport(nativeint board, int& transport, System.Text.StringBuilder note, int64 noteLen)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern nativeint gol_last_error()
 
 let check (what: string) rc =
@@ -58,5 +64,15 @@ type Board(width: int, height: int, boundary: Boundary, ?numGpus: int) =
         let w = Array.zeroCreate<uint64> (height * ((width + 63) / 64))
         check "gol_save_packed" (gol_save_packed(h, w, int64 w.Length)); w
     member _.Load(words: uint64[]) = check "gol_load_packed" (gol_load_packed(h, words, int64 words.Length))
+    /// Wait for the board's work; reports a failed cooperative pass (GOL_ERR_HIP) like every readback.
+    member _.Synchronize() = check "gol_synchronize" (gol_synchronize h)
+    /// Path / tuning option (gol.h lists the names, e.g. "coop" 0); results are bit-identical for every setting.
+    member this.SetOption(name: string, value: int64) =
+        check "gol_set_option" (gol_set_option(h, name, value)); this
+    /// Halo transport of a multi-GPU board: 0 none (one part), 1 peer copies, 2 RCCL; with the reason.
+    member _.Transport() =
+        let mutable t = 0
+        let note = System.Text.StringBuilder(256)
+        check "gol_transport" (gol_transport(h, &t, note, int64 note.Capacity)); (t, note.ToString())
     interface IDisposable with
         member _.Dispose() = if h <> 0n then (gol_destroy h |> ignore; h <- 0n)
