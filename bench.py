@@ -96,13 +96,17 @@ def parse():
                    "several ranks share one GPU in rehearsals)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--handle-leg-child", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--handle-timeout", type=float, default=180.0,
+    p.add_argument("--handle-timeout", type=float, default=300.0,
                    help="seconds the one-process handle leg (a child process of rank 0) may take")
     p.add_argument("--handle-parts", type=int, default=-1,
-                   help="one-process C-ABI leg (gol_create_multi, csrc/gol_multi.cpp: what the F# drop-in calls): "
-                   "the same board in P row strips on devices 0..P-1 (round-robin over the visible devices, so "
-                   "a one-GPU box rehearses it with every strip on device 0), timed by rank 0 after the main "
-                   "leg; -1 = the world size when N > 1, else off; 0 = off")
+                   help="one-process C-ABI leg (gol_create / gol_create_multi, csrc/gol_multi.cpp: what the F# "
+                   "drop-in calls, run without torch on the library's own HIP runtime): the same board in P row "
+                   "strips on devices 0..P-1 (round-robin over the visible devices, so a one-GPU box rehearses it "
+                   "with every strip on device 0), timed by rank 0 after the main leg and hashed at the main leg's "
+                   "verify generation; -1 = the world size (1: the single board); 0 = off")
+    p.add_argument("--verify-gen", type=int, default=-1, help=argparse.SUPPRESS)
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the untimed self-check (step to the next golden checkpoint and compare hashes)")
     return p.parse_args()
 
 
@@ -187,43 +191,76 @@ def cpu_baseline(args):
     }
 
 
-def handle_leg(args, W, H, boundary, parts, ndev):
-    """Time the one-process multi-GPU handle on the bench board: warmup passes, then args.steps passes of
-    its depth, host wall time around gol_step + gol_synchronize; then one pass with per-strip HIP timing
-    events (gol_pass_timing): interior launch, edge-band wait (halo peer copies landed), edge bands."""
+def _handle_run(args, W, H, boundary, devices, transport):
+    """One handle-leg board: warmup passes, args.steps timed passes of its depth (host wall time around gol_step +
+    gol_synchronize, and the library's own HIP events: gol_step_timed), then untimed to args.verify_gen and hashed."""
     from gameoflifewithactors_amd import Board
 
-    devices = [i % ndev for i in range(parts)]
-    with Board(W, H, boundary, devices=devices) as b:
+    parts = len(devices)
+    with Board(W, H, boundary, devices=devices if parts > 1 else None) as b:
+        if transport == "rccl":
+            b.set_option("transport", 2)  # raises when RCCL cannot serve this placement
         k = b.parts()[0]["ghost"] if parts > 1 else b.info()["tblock_k"]
-        transport = b.transport()
         b.seed_splitmix(args.seed)
         b.step(args.warmup * k)
         b.synchronize()
         t0 = time.perf_counter()
-        b.step(args.steps * k)
-        b.synchronize()
+        dev_us = b.step_timed(args.steps * k)
         dt = time.perf_counter() - t0
-        timing = b.pass_timing()
-    return {
-        "value": round(W * H * args.steps * k / dt / 1e9, 3),
-        "unit": "GCUPS",
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
-        "generations_per_step": k,
-        "strips": parts,
-        "devices": devices,
-        "transport": transport,
-        "pass_timing_us": timing,
-        "edge_wait_us_max": max(t["edge_wait_us"] for t in timing),
-    }
+        timing = b.pass_timing() if parts > 1 else None
+        out = {
+            "value": round(W * H * args.steps * k / dt / 1e9, 3),
+            "value_device_events": round(W * H * args.steps * k / (dev_us * 1e-6) / 1e9, 3),
+            "unit": "GCUPS",
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "avg_pass_us_device_events": round(dev_us / args.steps, 2),
+            "generations_per_step": k,
+            "transport": b.transport(),
+        }
+        if timing is not None:
+            out["pass_timing_us"] = timing
+            out["edge_wait_us_max"] = max(t["edge_wait_us"] for t in timing)
+        if args.verify_gen >= b.generation:
+            b.step(args.verify_gen - b.generation)
+            out["verify_generation"] = b.generation
+            out["hash"] = b.hash()
+            out["population"] = b.population()
+    return out
 
 
-def run_handle_leg(args, W, H, boundary, parts, ndev):
-    """The handle leg in a child process of rank 0 under a time limit: with N > 1 distinct GPUs it creates an RCCL
-    communicator over all of them inside one process, and a failure or hang there must not cost the main line."""
+def handle_leg(args, W, H, boundary, parts, ndev):
+    """The one-process C-ABI board (what the F# drop-in calls: gol_create / gol_create_multi, csrc/gol_multi.cpp) on
+    the bench board, in this child process WITHOUT torch, so the library runs on the HIP runtime it links
+    (/opt/rocm), as the F# host does.  parts = 1: the single board; parts > 1: row strips on devices 0..parts-1
+    (round-robin over the visible devices: a one-GPU box rehearses it with every strip on device 0), once with the
+    default peer-copy transport and, when every strip has its own GPU, once more over RCCL.  Each run reports its
+    rate and the board's hash at args.verify_gen (bench.py compares them with the main leg's)."""
+    from gameoflifewithactors_amd import _lib
+
+    devices = [i % ndev for i in range(parts)]
+    out = {"strips": parts, "devices": devices, "hip_runtime": None}
+    runs = {"single" if parts == 1 else "peer": None}
+    if parts > 1 and len(set(devices)) == parts:
+        runs["rccl"] = None
+    for name in runs:
+        try:
+            runs[name] = _handle_run(args, W, H, boundary, devices, name)
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the main leg stands
+            runs[name] = {"error": f"{type(e).__name__}: {e}"}
+    out["hip_runtime"] = _lib.hip_runtimes()
+    first = next(iter(runs))
+    out.update({k: v for k, v in runs[first].items()})  # the default transport's figures at the top level
+    out["runs"] = runs
+    return out
+
+
+def run_handle_leg(args, W, H, boundary, parts, verify_gen):
+    """The handle leg in a child process of rank 0 under a time limit: it may create an RCCL communicator over all
+    GPUs inside one process, and a failure or hang there must not cost the main line.  The child never imports
+    torch (bench.py main)."""
     cmd = [sys.executable, os.path.abspath(__file__), "--handle-leg-child", "--width", str(W), "--height", str(H),
            "--boundary", args.boundary, "--handle-parts", str(parts), "--steps", str(args.steps),
-           "--warmup", str(args.warmup), "--seed", str(args.seed)]
+           "--warmup", str(args.warmup), "--seed", str(args.seed), "--verify-gen", str(verify_gen)]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
@@ -257,11 +294,13 @@ def load_traffic(path, key, fingerprint):
 def board_leg(args) -> dict:
     """BASELINE configs 1, 2 and 5 on the C-ABI board (what the F# drop-in calls): the board the reference seeds
     (--init), one gol_step call of --gens-per-step generations per step, so the engine picks the pass it picks for
-    the size (single-wave, cooperative, LDS-resident or streaming).  Host wall time around the timed calls and HIP
-    events on the board's stream.  N = 1 only."""
-    import torch
-
-    from gameoflifewithactors_amd import BOUNDED, INIT_DOTNET_MOD2, INIT_DOTNET_NEXT2, TORUS, Board, patterns
+    the size (single-wave, cooperative, LDS-resident or streaming).  Host wall time around the timed calls, and the
+    device time of each call from the library's own HIP events (gol_step_timed).  N = 1 only.  This leg never imports
+    torch: the library runs on the HIP runtime it links (/opt/rocm), as under the F# host, and no torch object
+    outlives the board's stream (round 3's exit-time SIGSEGV: a torch ExternalStream around the board's stream,
+    destroyed by gol_destroy while torch still held it).  The final board is checked against the
+    golden_long.json checkpoint at its generation when one exists (configs 2 and 5)."""
+    from gameoflifewithactors_amd import BOUNDED, INIT_DOTNET_MOD2, INIT_DOTNET_NEXT2, TORUS, Board, checkpoints, patterns
 
     W, H = args.width, args.height
     boundary = TORUS if args.boundary == "torus" else BOUNDED
@@ -277,24 +316,28 @@ def board_leg(args) -> dict:
                 b.place_rle(text, x, y)
         else:
             raise SystemExit(f"unknown --init {args.init}")
-        h0 = b.hash()
+        h0, p0 = b.hash(), b.population()
         for _ in range(args.warmup):
             b.step(gps)
         b.synchronize()
         first = b.generation
-        s = torch.cuda.ExternalStream(b.stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dev_us = 0.0
         t0 = time.perf_counter()
-        e0.record(s)
         for _ in range(steps):
-            b.step(gps)
-        e1.record(s)
-        b.synchronize()
+            dev_us += b.step_timed(gps)
         dt = time.perf_counter() - t0
-        kernel_s = e0.elapsed_time(e1) / 1e3
+        kernel_s = dev_us * 1e-6
         info = b.info()
         end_hash, pop = b.hash(), b.population()
         gens = steps * gps
+        end_gen = b.generation
+    name, case = checkpoints.board_case(W, H, boundary, args.init, args.seed)
+    init_mark = checkpoints.initial_mark(case)
+    verify = checkpoints.verdict(end_gen, end_hash, pop, checkpoints.at_generation(case, end_gen),
+                                 f"tests/golden/golden_long.json[{name}]" if name else None)
+    if init_mark is not None:
+        verify["initial_ok"] = (h0, p0) == tuple(init_mark)
+        verify["ok"] = bool(verify["initial_ok"]) and verify["ok"] is not False
     return {
         "metric": "cell updates/sec (GCUPS) of gol_step on the C-ABI board",
         "value": round(W * H * gens / dt / 1e9, 3),
@@ -316,6 +359,7 @@ def board_leg(args) -> dict:
                    "generations_per_step": gps, "first_generation_timed": first, "generations_timed": gens,
                    "tblock_k": info["tblock_k"], "interleave": info["ilv"], "parallelism": "single board",
                    "initial_hash": f"{h0:016x}", "final_hash": f"{end_hash:016x}", "final_population": pop},
+        "verify": verify,
         "hip_runtime": _lib_runtimes(),
     }
 
@@ -328,22 +372,20 @@ def _lib_runtimes():
 
 def main():
     args = parse()
-    if args.handle_leg_child:  # rank 0's child process (run_handle_leg)
-        import torch
-
-        from gameoflifewithactors_amd import TORUS, BOUNDED
+    if args.handle_leg_child:  # rank 0's child process (run_handle_leg): no torch, the library's own runtime
+        from gameoflifewithactors_amd import TORUS, BOUNDED, _lib
 
         boundary = TORUS if args.boundary == "torus" else BOUNDED
         print(json.dumps(handle_leg(args, args.width, args.height, boundary, args.handle_parts,
-                                    torch.cuda.device_count())), flush=True)
+                                    _lib.device_count())), flush=True)
         return
     if args.init != "splitmix":
         if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
             raise SystemExit("--init other than splitmix times the single C-ABI board (N = 1)")
-        import torch
-
-        torch.cuda.set_device(0)
-        print(json.dumps(board_leg(args)), flush=True)
+        line = board_leg(args)
+        print(json.dumps(line), flush=True)
+        if line["verify"]["ok"] is False:
+            raise SystemExit("board differs from the golden checkpoint (verify.ok false)")
         return
     import torch
     import torch.distributed as dist
@@ -370,7 +412,7 @@ def main():
             dist.init_process_group("gloo", timeout=timeout)
             host_group = dist.group.WORLD
 
-    from gameoflifewithactors_amd import TORUS, BOUNDED
+    from gameoflifewithactors_amd import TORUS, BOUNDED, checkpoints
     from gameoflifewithactors_amd.strips import StripRunner
 
     from gameoflifewithactors_amd import _lib
@@ -494,17 +536,39 @@ def main():
     tr = (load_traffic(args.traffic_json, tkey, fingerprint) or {}) if world == 1 else {}
     traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)
 
+    # Self-check (untimed, after every timed and reference leg): step on to the first committed golden checkpoint
+    # at or after the generation the board reached and compare the all-reduced canonical hash and population
+    # (gameoflifewithactors_amd/checkpoints.py); every rank takes part in the reductions.
+    verify = None
+    verify_gen = -1
+    expected, source = None, None
+    got_hash = got_pop = None
+    if not args.no_verify:
+        cname, case = checkpoints.splitmix_case(W, H, boundary, args.seed)
+        expected = checkpoints.next_checkpoint(case, runner.generation)
+        source = f"tests/golden/golden_full.json[{cname}]" if expected else None
+        verify_gen = expected[0] if expected else runner.generation
+        runner.step(verify_gen - runner.generation)
+        torch.cuda.synchronize()
+        got_hash, got_pop = runner.hash(), runner.population()
+
     # One-process C-ABI leg (rank 0), after the main leg; the other ranks wait on a host barrier.
-    parts = args.handle_parts if args.handle_parts >= 0 else (world if world > 1 else 0)
+    parts = args.handle_parts if args.handle_parts >= 0 else world
     handle = None
     if parts >= 1:
         if world > 1:
             torch.cuda.synchronize()
             dist.barrier(group=host_group)
         if rank == 0:
-            handle = run_handle_leg(args, W, H, boundary, parts, torch.cuda.device_count())
+            handle = run_handle_leg(args, W, H, boundary, parts, verify_gen)
         if world > 1:
             dist.barrier(group=host_group)
+    if rank == 0 and got_hash is not None:
+        others = {}
+        for name, run in ((handle or {}).get("runs") or {}).items():
+            if isinstance(run, dict) and run.get("verify_generation") == verify_gen:
+                others[f"handle_leg.{name}"] = run.get("hash")
+        verify = checkpoints.verdict(verify_gen, got_hash, got_pop, expected, source, others)
 
     result = None
     if rank == 0:
@@ -565,6 +629,8 @@ def main():
             "hip_runtime": _lib.hip_runtimes(),
             "device_code": fingerprint,
         }
+        if verify is not None:
+            result["verify"] = verify
         if handle is not None:
             result["handle_leg"] = handle
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N = 1 figure (rank 0 only)
@@ -573,6 +639,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if verify is not None and verify["ok"] is False:
+        raise SystemExit("the timed board differs from its reference (verify.ok false)")
 
 
 if __name__ == "__main__":

@@ -121,6 +121,8 @@ SIGNATURES = {
     "gol_exchange_plan": (ctypes.c_int, [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, ctypes.POINTER(Xfer), i64,
                                          i64p]),
     "gol_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
+    "gol_device_count": (ctypes.c_int, [ip]),
+    "gol_step_timed": (ctypes.c_int, [vp, i64, ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -198,13 +200,39 @@ def _torch_runtime_first() -> None:
     """torch ships its own HIP runtime (torch/lib/libamdhip64.so, ROCm 7.0) under the same soname as the one
     libgol_hip.so links (/opt/rocm/lib/libamdhip64.so.7, ROCm 7.2), and the dynamic loader binds every later
     library to whichever was loaded first.  If libgol_hip.so came first, torch's own kernels ran on the 7.2
-    runtime and its lazy init failed ("No HIP GPUs are available", profiles/r2/pytest_parity_d.log).  So when
-    torch is importable it is imported BEFORE the library: the process then has one runtime, torch's, shared by
-    torch and libgol_hip.so.  A process without torch (the F# host, the C++ mirror) uses /opt/rocm's."""
-    try:
-        import torch  # noqa: F401  (loads torch's libamdhip64)
-    except Exception:  # torch absent or broken: the library brings its own runtime
-        pass
+    runtime and its lazy init failed ("No HIP GPUs are available", profiles/r2/pytest_parity_d.log).
+
+    So the rule is: a process that uses torch imports it BEFORE the library (then both share torch's runtime), and a
+    process without torch (the F# host, the C++ mirror, bench.py's handle leg) runs on /opt/rocm's.  load() does not
+    import torch itself (no torch import as a side effect of loading the library); when torch is
+    already imported it is already mapped, and when it is not, an import hook warns at a LATER `import torch` with
+    this explanation instead of leaving torch to fail at its first kernel."""
+    import sys
+
+    if "torch" in sys.modules:
+        return
+    sys.meta_path.insert(0, _TorchAfterLibrary())
+
+
+class _TorchAfterLibrary:
+    """sys.meta_path finder installed when libgol_hip.so was loaded without torch: importing torch afterwards binds
+    torch to /opt/rocm's HIP runtime, on which torch's own kernels fail ("No HIP GPUs are available").  It warns once,
+    at that import, with the reason (a RuntimeWarning rather than an ImportError: a host process that imports torch
+    only for bookkeeping keeps working, and the library itself is unaffected)."""
+
+    warned = False
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch" and not _TorchAfterLibrary.warned and _lib is not None:
+            rts = hip_runtimes()
+            if len(rts) == 1 and "/torch/" not in rts[0]:
+                import warnings
+
+                _TorchAfterLibrary.warned = True
+                warnings.warn("torch imported after gameoflifewithactors_amd loaded libgol_hip.so on " + rts[0] +
+                              ": torch's kernels cannot run on that HIP runtime; import torch before the library",
+                              RuntimeWarning, stacklevel=2)
+        return None
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -218,7 +246,6 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             f"{path} not found: build it with `python -m gameoflifewithactors_amd.build` "
             "(there is no CPU fallback for the hot path)"
         )
-    _torch_runtime_first()
     lib = ctypes.CDLL(path)
     rts = hip_runtimes()
     if len(rts) > 1:
@@ -229,7 +256,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    _torch_runtime_first()
     return lib
+
+
+def device_count() -> int:
+    """HIP devices visible to the library (gol_device_count; no torch needed)."""
+    n = ctypes.c_int()
+    check(load().gol_device_count(ctypes.byref(n)), "gol_device_count")
+    return n.value
 
 
 def exchange_plan(height: int, boundary: int, nparts: int, ghost: int, k: int) -> list:

@@ -32,7 +32,7 @@ class Board:
     boundary: ``TORUS`` (the actors' topology, GameOfLifeDriver.fs:25) or ``BOUNDED`` (Script.fsx:11).
     tblock_k: upper bound on the generations fused per kernel pass (0 = library default).
     num_gpus: N > 1 spreads the board over devices 0..N-1 of this process as row strips with peer-copied
-              halo rows (``gol_create``; bit-identical to one GPU).
+              halo rows (``gol_create``; bit-identical to one GPU; option {"transport": 2} moves them by RCCL).
     devices: explicit strip placement (``gol_create_multi``), e.g. ``[0, 0, 0]`` runs three strips on one GPU.
     ilv: packed layout, words per interleaved block (0 = library default for the width; 1, 2, 4).
     options: {name: value} passed to gol_set_option after creation (e.g. {"coop": 0}).
@@ -51,8 +51,12 @@ class Board:
                   "gol_create")
         self._h = h
         self.width, self.height, self.boundary = width, height, boundary
-        for name, value in (options or {}).items():
-            self.set_option(name, value)
+        try:
+            for name, value in (options or {}).items():
+                self.set_option(name, value)
+        except Exception:
+            self.close()
+            raise
 
     # ---------------------------------------------------------------- lifetime
     def close(self) -> None:
@@ -164,6 +168,13 @@ class Board:
     def step(self, generations: int = 1) -> "Board":
         check(self._lib.gol_step(self._h, generations), "gol_step")
         return self
+
+    def step_timed(self, generations: int) -> float:
+        """gol_step between HIP timing events on the board's stream, synchronised (gol_step_timed): the call's device
+        time in microseconds, measured by the HIP runtime the library itself runs on."""
+        us = ctypes.c_double()
+        check(self._lib.gol_step_timed(self._h, generations, ctypes.byref(us)), "gol_step_timed")
+        return us.value
 
     def synchronize(self) -> None:
         check(self._lib.gol_synchronize(self._h), "gol_synchronize")

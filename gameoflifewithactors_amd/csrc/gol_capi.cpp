@@ -316,11 +316,24 @@ int sync(gol_board* b) {
 }
 
 // The board's cells were replaced as a whole: a timed-out hand-off no longer matters, and a ragged board's scratch
-// rows no longer hold its state.
+// rows no longer hold its state.  The stream is drained first (the overwrite was queued behind any earlier pass),
+// then the cooperative error word is cleared WITHOUT marking the board invalid: an error a timed-out pass left
+// there, with no readback or gol_synchronize after it, must not fail the overwrite that replaces its result
+// (tests/test_gpu_coop.py::test_coop_timeout_then_overwrite_without_readback).
 int overwritten(gol_board* b) {
+    if (b->multi) {
+        b->invalid = false;
+        b->rag_state = 0;
+        return b->multi->synchronize();
+    }
+    GOL_HIP(hipStreamSynchronize(b->stream));
+    if (b->coop) {
+        GOL_HIP(hipMemsetAsync(b->coop + kCoopErrWord, 0, sizeof(unsigned), b->stream));
+        GOL_HIP(hipStreamSynchronize(b->stream));
+    }
     b->invalid = false;
     b->rag_state = 0;
-    return sync(b);
+    return GOL_OK;
 }
 
 // A ragged byte board whose state the multi-generation passes left in the scratch rows (rag_state): unpack it into
@@ -688,7 +701,68 @@ int check_strip(const gol_strip* s) {
     return GOL_OK;
 }
 
+// StreamArgs of a strip pass (gol_strip_step / gol_strip_plan and the multi board's launches)
+gol::StreamArgs strip_args(const gol_strip* s, int64_t out_begin, int64_t out_end, int32_t split_opt, int64_t seg_opt,
+                           int32_t seam_opt) {
+    gol::StreamArgs a{};
+    a.words = s->width / 32;
+    a.pitch = s->pitch;
+    a.rows = s->rows;
+    a.ghost = s->ghost;
+    a.y0 = s->y0;
+    a.height = s->height;
+    a.out_begin = out_begin;
+    a.out_end = out_end;
+    a.seg = 0;
+    a.ilv = s->ilv;
+    a.spare = s->spare_waves > 0 ? s->spare_waves : 0;
+    a.split_opt = split_opt;
+    a.seg_opt = seg_opt;
+    a.seam_opt = seam_opt;
+    return a;
+}
+
 }  // namespace
+
+namespace gol {
+
+int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows,
+                    int32_t split_opt, int64_t seg_opt, int32_t seam_opt) {
+    if (int rc = check_strip(s)) return rc;
+    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt);
+    gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
+    if (seg_rows) *seg_rows = a.seg;
+    if (waves)
+        *waves = (a.nstrips * a.nsegs + a.rem_units) *
+                 (a.split > 0 ? gol::stream_wpb(a.words, k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
+    return GOL_OK;
+}
+
+int strip_step_opts(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin, int64_t out_end,
+                    hipStream_t stream, int32_t split_opt, int64_t seg_opt, int32_t seam_opt) {
+    if (int rc = check_strip(s)) return rc;
+    if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
+    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    if (out_begin == out_end) return GOL_OK;
+    if (!s->wrap_rows) {
+        // every row the pass can read must exist in the buffer, except rows beyond a bounded board's edge
+        int64_t lo = out_begin - k, hi = out_end + k;
+        if (s->boundary == GOL_BOUNDED) {
+            lo = std::max<int64_t>(lo, -s->y0);
+            hi = std::min<int64_t>(hi, s->height - s->y0);
+        }
+        if (lo < -s->ghost || hi > s->rows + s->ghost)
+            return fail(GOL_ERR_INVALID, "pass reads rows outside the buffer: ghost must be >= k");
+    }
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt);
+    GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0, stream));
+    return GOL_OK;
+}
+
+}  // namespace gol
 
 extern "C" {
 
@@ -1214,6 +1288,12 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         o.split = (int32_t)(value < 0 ? -1 : value);
     } else if (n == "seg_rows") o.seg_rows = value < 0 ? 0 : value;
     else if (n == "seam") o.seam = value < 0 ? -1 : 0;
+    else if (n == "transport") {
+        // multi-part boards: 1 = peer copies (the default), 2 = RCCL (distinct devices only)
+        if (!b->multi) return fail(GOL_ERR_UNSUPPORTED, "transport: a single board has no halo exchange");
+        DeviceGuard dg(b->device);
+        return b->multi->set_transport((int)value);
+    }
     else if (n == "ragged_stream") o.ragged_stream = value != 0;
     else if (n == "coop_r") {
         if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
@@ -1232,6 +1312,8 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (b->coop_xch) b->coop_epoch = (unsigned)value;
     } else
         return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
+    // a multi-part board runs every strip launch with the streaming options (the other passes never run there)
+    if (b->multi) b->multi->set_stream_options(o.split, o.seg_rows, o.seam);
     return GOL_OK;
 }
 
@@ -1255,9 +1337,47 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
     else if (n == "resident_threads") *value = o.resident_threads;
     else if (n == "coop_epoch") *value = b->coop_epoch;
+    else if (n == "transport") *value = b->multi ? b->multi->transport() : GOL_TRANSPORT_NONE;
     else
         return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
     return GOL_OK;
+}
+
+int gol_device_count(int* n) {
+    if (!n) return fail(GOL_ERR_INVALID, "null argument");
+    *n = 0;
+    int c = 0;
+    const hipError_t e = hipGetDeviceCount(&c);
+    if (e == hipErrorNoDevice) return GOL_OK;
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *n = c;
+    return GOL_OK;
+}
+
+int gol_step_timed(gol_board* b, int64_t generations, double* elapsed_us) {
+    if (int rc = check_board(b)) return rc;
+    if (!elapsed_us) return fail(GOL_ERR_INVALID, "null elapsed_us");
+    std::lock_guard<std::mutex> g(b->mu);
+    DeviceGuard dg(b->device);
+    if (generations < 0) return fail(GOL_ERR_INVALID, "negative generations");
+    if (b->multi) return b->multi->step_timed(generations, &b->generation, elapsed_us);
+    // before the first event: a ragged board's byte state the call would not use is settled like in gol_step
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    GOL_HIP(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    int rc = GOL_OK;
+    if (e == hipSuccess) e = hipEventRecord(e0, b->stream);
+    if (e == hipSuccess) rc = step_impl(b, generations);
+    if (e == hipSuccess && rc == GOL_OK) e = hipEventRecord(e1, b->stream);
+    if (e == hipSuccess && rc == GOL_OK) e = hipEventSynchronize(e1);
+    float ms = 0;
+    if (e == hipSuccess && rc == GOL_OK) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (rc != GOL_OK) return rc;
+    if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("step timing: ") + hipGetErrorString(e));
+    *elapsed_us = 1e3 * ms;
+    return check_valid(b);
 }
 
 int gol_stream(gol_board* b, void** stream) {
@@ -1268,60 +1388,12 @@ int gol_stream(gol_board* b, void** stream) {
 
 // ---------------------------------------------------------------- row strips
 int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows) {
-    if (int rc = check_strip(s)) return rc;
-    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
-    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
-    gol::StreamArgs a{};
-    a.words = s->width / 32;
-    a.pitch = s->pitch;
-    a.rows = s->rows;
-    a.ghost = s->ghost;
-    a.y0 = s->y0;
-    a.height = s->height;
-    a.out_begin = out_begin;
-    a.out_end = out_end;
-    a.ilv = s->ilv;
-    a.spare = s->spare_waves > 0 ? s->spare_waves : 0;
-    gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
-    if (seg_rows) *seg_rows = a.seg;
-    if (waves)
-        *waves = (a.nstrips * a.nsegs + a.rem_units) *
-                 (a.split > 0 ? gol::stream_wpb(a.words, k, s->ilv, s->boundary == GOL_BOUNDED, s->wrap_rows != 0) / 4 : 1);
-    return GOL_OK;
+    return gol::strip_plan_opts(s, k, out_begin, out_end, waves, seg_rows, 0, 0, 0);
 }
 
 int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin,
                    int64_t out_end, void* stream) {
-    if (int rc = check_strip(s)) return rc;
-    if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
-    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
-    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
-    if (out_begin == out_end) return GOL_OK;
-    if (!s->wrap_rows) {
-        // every row the pass can read must exist in the buffer, except rows beyond a bounded board's edge
-        int64_t lo = out_begin - k, hi = out_end + k;
-        if (s->boundary == GOL_BOUNDED) {
-            lo = std::max<int64_t>(lo, -s->y0);
-            hi = std::min<int64_t>(hi, s->height - s->y0);
-        }
-        if (lo < -s->ghost || hi > s->rows + s->ghost)
-            return fail(GOL_ERR_INVALID, "pass reads rows outside the buffer: ghost must be >= k");
-    }
-    gol::StreamArgs a{};
-    a.words = s->width / 32;
-    a.pitch = s->pitch;
-    a.rows = s->rows;
-    a.ghost = s->ghost;
-    a.y0 = s->y0;
-    a.height = s->height;
-    a.out_begin = out_begin;
-    a.out_end = out_end;
-    a.seg = 0;
-    a.ilv = s->ilv;
-    a.spare = s->spare_waves > 0 ? s->spare_waves : 0;
-    GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0,
-                                    (hipStream_t)stream));
-    return GOL_OK;
+    return gol::strip_step_opts(s, src, dst, k, out_begin, out_end, (hipStream_t)stream, 0, 0, 0);
 }
 
 int gol_strip_seed_splitmix(const gol_strip* s, uint32_t* buf, uint64_t seed, void* stream) {

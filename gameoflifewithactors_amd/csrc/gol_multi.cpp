@@ -4,8 +4,8 @@
 // the dictionary of cell actors built by GameOfLifeDriver.fs:16-30 and ticked by updateView (L32-34).
 // The per-pass protocol (ghost rows of depth k, interior || exchange, then the edge bands) is the one the
 // one-process-per-GPU path runs over torch.distributed (strips.py).  Here one process drives every part: the
-// exchange is RCCL send/recv over a communicator spanning the parts' devices (ncclCommInitAll) when every part
-// has its own GPU, or a peer copy ordered by HIP events when a device repeats (the one-GPU rehearsal).
+// exchange is a peer copy ordered by HIP events (the default), or on request (gol_set_option "transport") RCCL
+// send/recv over a communicator spanning the parts' devices (ncclCommInitAll) when every part has its own GPU.
 #include "gol_multi.h"
 
 #include <dlfcn.h>
@@ -104,25 +104,44 @@ std::vector<gol_xfer> exchange_plan(int64_t height, int boundary, int nparts, in
     return ops;
 }
 
+// Creates the RCCL communicators (once); GOL_ERR_UNSUPPORTED with the reason when RCCL cannot serve this board.
 int MultiBoard::init_rccl() {
+    if (comms_) return GOL_OK;
+    if (!distinct_) return api_fail(GOL_ERR_UNSUPPORTED, "RCCL transport: a device holds more than one part (RCCL needs "
+                                                         "one rank per GPU)");
     const Rccl& nc = Rccl::get();
-    if (!nc.ok()) {
-        transport_note_ = "peer copies: " + nc.error;
-        return GOL_OK;
-    }
+    if (!nc.ok()) return api_fail(GOL_ERR_UNSUPPORTED, "RCCL transport: " + nc.error);
     std::vector<int> devs;
     for (const Part& p : parts_) devs.push_back(p.device);
     std::vector<ncclComm_t> comms(parts_.size(), nullptr);
     const ncclResult_t r = nc.init_all(comms.data(), (int)devs.size(), devs.data());
-    if (r != ncclSuccess) {
-        transport_note_ = "peer copies: ncclCommInitAll failed: " + nc.why(r);
-        return GOL_OK;
-    }
+    if (r != ncclSuccess) return api_fail(GOL_ERR_UNSUPPORTED, "RCCL transport: ncclCommInitAll failed: " + nc.why(r));
     for (size_t i = 0; i < parts_.size(); i++) parts_[i].comm = comms[i];
-    rccl_ = true;
-    transport_note_ = "RCCL ncclSend/ncclRecv over one communicator per part (ncclCommInitAll, " +
-                      std::to_string(parts_.size()) + " devices)";
+    comms_ = true;
     return GOL_OK;
+}
+
+int MultiBoard::set_transport(int transport) {
+    if (transport != GOL_TRANSPORT_PEER && transport != GOL_TRANSPORT_RCCL)
+        return api_fail(GOL_ERR_INVALID, "transport must be 1 (peer copies) or 2 (RCCL)");
+    GOL_MRC(synchronize());  // no pass of the old transport is in flight
+    if (transport == GOL_TRANSPORT_RCCL) {
+        GOL_MRC(init_rccl());
+        rccl_ = true;
+        transport_note_ = "RCCL ncclSend/ncclRecv over one communicator per part (ncclCommInitAll, " +
+                          std::to_string(parts_.size()) + " devices)";
+    } else {
+        rccl_ = false;
+        transport_note_ = distinct_ ? "peer copies: hipMemcpyPeerAsync between the parts' devices (the default)"
+                                    : "peer copies: a device holds more than one part (RCCL needs one rank per GPU)";
+    }
+    return GOL_OK;
+}
+
+// gol_strip_step with the board's streaming options (gol_capi.cpp)
+int MultiBoard::strip_step(const gol_strip& s, const uint32_t* src, uint32_t* dst, int k, int64_t b, int64_t e,
+                           hipStream_t st) const {
+    return strip_step_opts(&s, src, dst, k, b, e, st, split_opt_, seg_opt_, seam_opt_);
 }
 
 int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock, int ilv) {
@@ -173,18 +192,16 @@ int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* dev
         }
         GOL_MHIP(hipMalloc(&p.acc, 64));
     }
-    // RCCL when every part has its own device; peer copies when a device repeats (RCCL refuses two ranks on one GPU)
+    // peer copies by default; RCCL on request (set_transport) when every part has its own device
     std::vector<int> seen;
-    bool distinct = true;
+    distinct_ = true;
     for (const Part& p : parts_) {
-        if (std::find(seen.begin(), seen.end(), p.device) != seen.end()) distinct = false;
+        if (std::find(seen.begin(), seen.end(), p.device) != seen.end()) distinct_ = false;
         seen.push_back(p.device);
     }
-    if (distinct) {
-        GOL_MRC(init_rccl());
-    } else {
-        transport_note_ = "peer copies: a device holds more than one part (RCCL needs one rank per GPU)";
-    }
+    rccl_ = false;
+    transport_note_ = distinct_ ? "peer copies: hipMemcpyPeerAsync between the parts' devices (the default)"
+                                : "peer copies: a device holds more than one part (RCCL needs one rank per GPU)";
     // peer access between neighbouring parts on distinct devices (xGMI); without it the copies are staged
     for (const Part& p : parts_)
         for (int q : {p.up, p.down}) {
@@ -437,11 +454,11 @@ int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
         if (lo < hi) {
             // leave room on the device for the two edge bands, which start as soon as the ghost rows land
             int64_t w0 = 0, w1 = 0;
-            GOL_MRC(gol_strip_plan(&p.s, k, 0, lo, &w0, nullptr));
-            GOL_MRC(gol_strip_plan(&p.s, k, hi, rows, &w1, nullptr));
+            GOL_MRC(strip_plan_opts(&p.s, k, 0, lo, &w0, nullptr, split_opt_, seg_opt_, seam_opt_));
+            GOL_MRC(strip_plan_opts(&p.s, k, hi, rows, &w1, nullptr, split_opt_, seg_opt_, seam_opt_));
             gol_strip s = p.s;
             s.spare_waves = (int32_t)std::min<int64_t>(w0 + w1, 1 << 20);
-            GOL_MRC(gol_strip_step(&s, src, dst, k, lo, hi, p.compute));
+            GOL_MRC(strip_step(s, src, dst, k, lo, hi, p.compute));
         }
         if (timers) GOL_MHIP(hipEventRecord((*timers)[i].interior, p.compute));
         GOL_MHIP(hipStreamWaitEvent(p.edge, p.ev_start, 0));
@@ -452,8 +469,8 @@ int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
                 if (q >= 0) GOL_MHIP(hipStreamWaitEvent(p.edge, parts_[(size_t)q].ev_copied, 0));
         }
         if (timers) GOL_MHIP(hipEventRecord((*timers)[i].go, p.edge));
-        GOL_MRC(gol_strip_step(&p.s, src, dst, k, 0, lo, p.edge));
-        GOL_MRC(gol_strip_step(&p.s, src, dst, k, hi, rows, p.edge));
+        GOL_MRC(strip_step(p.s, src, dst, k, 0, lo, p.edge));
+        GOL_MRC(strip_step(p.s, src, dst, k, hi, rows, p.edge));
         if (timers) GOL_MHIP(hipEventRecord((*timers)[i].edge, p.edge));
         GOL_MHIP(hipEventRecord(p.ev_edge, p.edge));
         GOL_MHIP(hipStreamWaitEvent(p.compute, p.ev_edge, 0));
@@ -493,6 +510,37 @@ int MultiBoard::timed_pass(double* interior_us, double* wait_us, double* edge_us
     }
     if (rc == GOL_OK) *done += max_k_;
     destroy();
+    return rc;
+}
+
+int MultiBoard::step_timed(int64_t generations, int64_t* done, double* elapsed_us) {
+    // events of one device are only comparable with each other: each part times its own span (first to last
+    // launch of the call on its compute stream, which joins its edge stream at the end of every pass)
+    std::vector<hipEvent_t> ev(2 * parts_.size(), nullptr);
+    int rc = GOL_OK;
+    for (size_t i = 0; i < parts_.size() && rc == GOL_OK; i++) {
+        if (hipSetDevice(parts_[i].device) != hipSuccess || hipEventCreate(&ev[2 * i]) != hipSuccess ||
+            hipEventCreate(&ev[2 * i + 1]) != hipSuccess || hipEventRecord(ev[2 * i], parts_[i].compute) != hipSuccess)
+            rc = api_fail(GOL_ERR_HIP, "step timing: event setup failed");
+    }
+    if (rc == GOL_OK) rc = step(generations, done);
+    double worst = 0;
+    for (size_t i = 0; i < parts_.size() && rc == GOL_OK; i++) {
+        float ms = 0;
+        if (hipSetDevice(parts_[i].device) != hipSuccess || hipEventRecord(ev[2 * i + 1], parts_[i].compute) != hipSuccess ||
+            hipEventSynchronize(ev[2 * i + 1]) != hipSuccess || hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) != hipSuccess)
+            rc = api_fail(GOL_ERR_HIP, "step timing: event readout failed");
+        worst = std::max(worst, 1e3 * (double)ms);
+    }
+    for (size_t i = 0; i < parts_.size(); i++) {
+        (void)hipSetDevice(parts_[i].device);
+        for (int j = 0; j < 2; j++)
+            if (ev[2 * i + j]) (void)hipEventDestroy(ev[2 * i + j]);
+    }
+    if (rc == GOL_OK) {
+        rc = synchronize();
+        *elapsed_us = worst;
+    }
     return rc;
 }
 

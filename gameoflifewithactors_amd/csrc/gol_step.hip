@@ -1146,6 +1146,10 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         // without a wrap (a single board's last segment shorter than k would push its neighbour's halo past it)
         int64_t mid = a.nsegs - 2;
         if (wrap && a.nsegs >= 3 && rows - (a.nsegs - 1) * seg < k) mid = a.nsegs - 3;
+        // sub-strip j streams rows [(j + 1) seg - k, (j + 2) seg + k) of the buffer at a fixed offset from
+        // sub-strip 0's walk: a segment shorter than k (the "seg_rows" option can ask for one) would make segment 1's
+        // first rows wrap or leave the buffer, so such segments run as lone remainder units
+        if (seg < k) mid = 0;
         a.rem_mid = mid > 0 ? mid : 0;
         a.rem_units = seam_rem_units(a, a.nsegs, a.rem_mid);
     }

@@ -49,14 +49,25 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  * boundary: GOL_TORUS (actors, GameOfLifeDriver.fs:25) or GOL_BOUNDED (Script.fsx:11).
  * num_gpus: 1 = one board on the calling thread's current device.  N > 1 = row strips on devices
  *           0..N-1 of THIS process (the reference host is one process, GameOfLifeDriver.fs:13-41): strip r
- *           owns rows [H*r/N, H*(r+1)/N); every pass copies k halo rows between neighbouring strips
- *           (hipMemcpyPeerAsync over xGMI) while the interior rows compute.  Needs width % 32 == 0.
- *           Bit-identical to num_gpus = 1.  (One process per GPU instead: gol_strip_* below.)
+ *           owns rows [H*r/N, H*(r+1)/N); every pass moves k halo rows between neighbouring strips while the
+ *           interior rows compute.  Halo transport: peer copies (hipMemcpyPeerAsync, xGMI between GPUs) by
+ *           default; RCCL send/recv on request (gol_set_option "transport" = 2, distinct devices only;
+ *           gol_transport reports which one runs).  Needs width % 32 == 0.  Bit-identical to num_gpus = 1.
+ *           (One process per GPU instead: gol_strip_* below.)
  * tblock_k: upper bound on the generations fused per kernel pass (0 = the engine's default for the
- *           board: latency-bound boards below 2^25 cells get ilv 1 and k = 8; larger ones ilv 2 and k = 16,
- *           k = 12 from 2^29 cells on a torus (single GPU or strips); bounded boards k = 16; else one of
- *           1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k).
- *           gol_layout / gol_info report the choice.
+ *           board, gol_layout / gol_info report it):
+ *             packed boards below 2^25 cells: ilv 1, k = 8 (latency-bound: the single-wave pass takes boards up
+ *               to 128 x 256), except single boards the cooperative pass takes (2^17 < cells <=
+ *               2^26, 4096 or 8192 wide): ilv 2 / 4 (that pass's words per lane) and k = 16 / 8, of
+ *               which it hands off every min(k, 8) generations;
+ *             packed boards of 2^25 .. 2^29 cells, width % 64 == 0: ilv 2, k = 16;
+ *             packed boards from 2^29 cells, width % 64 == 0: ilv 2, k = 12 -- torus and bounded alike
+ *               (bounded boards ran k = 16 until round 3), single board or strips;
+ *             other packed widths from 2^25 cells: ilv 1, k = 32;
+ *             byte boards (width % 32 != 0, ilv 0): k = 8 below 2^25 cells, 16 below 2^27, else 24;
+ *           else one of 1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k.
+ *           A multi-part board's halo depth (gol_part_info ghost) is the deepest supported k <= tblock_k that
+ *           fits its thinnest strip.
  * The initial board is all dead. */
 int gol_create(int64_t width, int64_t height, int boundary, int num_gpus, int tblock_k, gol_board** out);
 /* As gol_create with an explicit packed layout: ilv = 0 (auto, gol_default_ilv) or 1, 2, 4 words per
@@ -71,9 +82,10 @@ int gol_create_multi(int64_t width, int64_t height, int boundary, const int* dev
  * first global row, owned rows and halo depth (ghost rows per side; 0 for a single board). */
 int gol_num_parts(gol_board* b, int* n);
 int gol_part_info(gol_board* b, int part, int* device, int64_t* y0, int64_t* rows, int64_t* ghost);
-/* How a multi-part board moves its halo rows: RCCL send/recv (ncclCommInitAll over the parts' devices, xGMI) when
- * every part has its own device, else peer copies (a device repeats: RCCL refuses two ranks on one GPU); a
- * single board has none.  note (may be NULL, >= 256 bytes): why, e.g. the RCCL error that made it fall back. */
+/* How a multi-part board moves its halo rows: peer copies (the default) or RCCL send/recv (ncclCommInitAll over
+ * the parts' devices, xGMI) once gol_set_option(b, "transport", GOL_TRANSPORT_RCCL) succeeded -- it fails with
+ * GOL_ERR_UNSUPPORTED when a device repeats (RCCL refuses two ranks on one GPU) or RCCL is unavailable, and the
+ * board keeps peer copies.  A single board has none.  note (may be NULL, >= 256 bytes): a description. */
 enum { GOL_TRANSPORT_NONE = 0, GOL_TRANSPORT_PEER = 1, GOL_TRANSPORT_RCCL = 2 };
 int gol_transport(gol_board* b, int* transport, char* note, int64_t note_len);
 int gol_destroy(gol_board* b);
@@ -111,6 +123,10 @@ int gol_clear(gol_board* b);
 int gol_step(gol_board* b, int64_t generations);
 int gol_generation(gol_board* b, int64_t* out);
 int gol_synchronize(gol_board* b);
+/* Profiling: gol_step between two HIP timing events on the board's stream, then synchronise; *elapsed_us = the
+ * device time of the call (multi-part boards: each part times its own compute stream, the longest is reported).
+ * Lets a host without any other GPU runtime (the F# driver) time the engine under the HIP runtime it loads. */
+int gol_step_timed(gol_board* b, int64_t generations, double* elapsed_us);
 
 /* Replaces the render agent's pixel fill (GameOfLifeUI.fs:24-28; GameofLife.fs:53-57; Script.fsx:33-35):
  * pixels[x + y*stride] = alive ? alive_value : 0, stride >= width, buffer >= stride*height bytes. */
@@ -128,6 +144,8 @@ int gol_layout(gol_board* b, int* ilv, int64_t* pitch);
  * 32; boards below 2^25 cells use ilv 1, see gol_create), the default temporal-block depth for a layout
  * on a large board, and whether the step kernel supports depth k for a layout. */
 int gol_default_ilv(int64_t width);
+/* HIP devices visible to this process (0 and GOL_OK when there is none). */
+int gol_device_count(int* n);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller (multi-GPU
@@ -153,6 +171,9 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *                                (0: the measured default, -1: no split)
  *   "seg_rows" 0 | n             streaming pass: rows per wave segment (0: planned)
  *   "seam" 0 | -1                streaming pass on a torus: seam strips where they apply (-1: halo-lane strips)
+ *   "transport" 1 | 2            multi-part boards: halo rows by peer copies (1) or RCCL (2, distinct devices;
+ *                                GOL_ERR_UNSUPPORTED otherwise); GOL_ERR_UNSUPPORTED on a single board
+ *   ("split", "seg_rows" and "seam" apply to every strip launch of a multi-part board as well)
  *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
  *                                words (0: the per-generation byte step)
  *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments

@@ -9,6 +9,10 @@ import sys
 
 import pytest
 
+# torch first: it brings its own HIP runtime, which libgol_hip.so then shares (gameoflifewithactors_amd/_lib.py
+# _torch_runtime_first); loading the library first would make a later `import torch` fail by design
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE = os.path.join(ROOT, "oracle")
 for p in (ROOT, ORACLE):

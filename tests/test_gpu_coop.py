@@ -133,6 +133,26 @@ def test_coop_timeout_reported_on_every_readback(gol, oracle):
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 37, 0))
 
 
+def test_coop_timeout_then_overwrite_without_readback(gol, oracle):
+    """a cooperative pass that timed out, with NO readback or gol_synchronize after it, then an
+    overwrite: the overwrite must succeed (the stale error word is cleared without marking the board invalid) and
+    the board must read back valid and exact."""
+    b0 = _rand(2048, 2048, 92)
+    with gol.Board(2048, 2048, 0, options={"coop": 1, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
+        b.set_cells(b0)
+        for _ in range(5):  # nothing reads the error word in between
+            b.step(200)
+        b.set_option("coop_spin_limit", 0)
+        for overwrite in (lambda: b.set_cells(b0), lambda: b.load_packed(oracle.pack64(b0)),
+                          lambda: b.seed_splitmix(3) and b.set_cells(b0)):
+            b.set_option("coop_spin_limit", 1)
+            b.step(200)
+            b.set_option("coop_spin_limit", 0)
+            overwrite()  # must not raise
+            b.step(37)
+            np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 37, 0))
+
+
 @pytest.mark.parametrize("boundary", [0, 1])
 @pytest.mark.parametrize("w,h", [(129, 300), (1001, 257), (2047, 90), (2049, 131), (4095, 64), (4097, 77),
                                  (8191, 40), (333, 1000)])

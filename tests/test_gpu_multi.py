@@ -169,3 +169,32 @@ def test_transport_on_one_gpu_is_peer_copies(gol):
         assert b.transport().startswith("peer:"), b.transport()
     with gol.Board(1024, 256, 0) as b:
         assert b.transport().startswith("none:")
+
+
+@pytest.mark.parametrize("transport", [1, 2])
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_distinct_devices_both_transports_match_oracle(gol, oracle, transport, boundary):
+    """A node: one strip per GPU, halo rows by peer copies (the default) and by RCCL (transport 2),
+    bit-exact against the oracle and reporting the transport it runs.  Skipped on a one-GPU box."""
+    n = gol._lib.device_count()
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    w, h, gens = 1024, 40 * n, 45
+    b0 = _rand(h, w, 900 + transport + boundary)
+    with gol.Board(w, h, boundary, tblock_k=16, devices=list(range(n)), options={"transport": transport}) as b:
+        assert b.transport().startswith("rccl:" if transport == 2 else "peer:"), b.transport()
+        b.set_cells(b0).step(gens)
+        np.testing.assert_array_equal(b.get_cells(), oracle.run(b0, gens, boundary))
+
+
+@pytest.mark.parametrize("opts", [{"split": -1}, {"seg_rows": 20}, {"seam": -1}])
+def test_stream_options_reach_the_strip_launches(gol, oracle, opts):
+    """"split", "seg_rows" and "seam" apply to every strip launch of a multi-part board (they were
+    silently dropped); results stay exact."""
+    w, h, gens = 64 * 140, 300, 29
+    b0 = _rand(h, w, 31)
+    with gol.Board(w, h, 0, tblock_k=12, ilv=2, devices=[0, 0, 0], options=opts) as b:
+        for name, value in opts.items():
+            assert b.get_option(name) == value
+        b.set_cells(b0).step(gens)
+        np.testing.assert_array_equal(b.get_cells(), oracle.run(b0, gens, 0))

@@ -72,3 +72,19 @@ def test_seam_ghost_row_strips(gol, oracle):
     lb.set_cells(torch.as_tensor(b0))
     lb.step(3 * k + 1)
     np.testing.assert_array_equal(lb.get_cells().numpy(), oracle.c_run(b0, 3 * k + 1, 0))
+
+
+@pytest.mark.parametrize("seg_rows", [4, 8, 11])
+def test_seam_segments_shorter_than_k(gol, oracle, seg_rows):
+    """segments shorter than k (the "seg_rows" option accepts any length) must not be packed into
+    remainder waves -- sub-strip j reads its rows at a fixed offset from sub-strip 0's walk, so segment 1's first
+    rows would wrap.  Such segments run as lone remainder units; the board is still exact, on the single board and on
+    the ghost-row strips of a multi-part board (whose strip launches take the board's options too)."""
+    w, h, k = 64 * (63 * 2 + 16), 150, 12
+    b0 = _rand(h, w, 300 + seg_rows)
+    want = oracle.c_run(b0, 2 * k + 5, 0)
+    np.testing.assert_array_equal(_run(gol, b0, k, 2, {"seg_rows": seg_rows}), want)
+    with gol.Board(w, h, gol.TORUS, tblock_k=k, ilv=2, devices=[0, 0], options={"seg_rows": seg_rows}) as b:
+        assert b.get_option("seg_rows") == seg_rows
+        b.set_cells(b0).step(2 * k + 5)
+        np.testing.assert_array_equal(b.get_cells(), want)
