@@ -42,6 +42,10 @@ extern int gol_set_option(nativeint board, [<MarshalAs(UnmanagedType.LPStr)>] st
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern int gol_transport(nativeint board, int& transport, System.Text.StringBuilder note, int64 noteLen)
 [<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_step_timed(nativeint board, int64 generations, double& elapsedUs)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
+extern int gol_device_count(int& n)
+[<DllImport(Lib, CallingConvention = CallingConvention.Cdecl)>]
 extern nativeint gol_last_error()
 
 let check (what: string) rc =
@@ -64,12 +68,18 @@ type Board(width: int, height: int, boundary: Boundary, ?numGpus: int) =
         let w = Array.zeroCreate<uint64> (height * ((width + 63) / 64))
         check "gol_save_packed" (gol_save_packed(h, w, int64 w.Length)); w
     member _.Load(words: uint64[]) = check "gol_load_packed" (gol_load_packed(h, words, int64 words.Length))
+    /// gol_step timed by the library's own HIP events (device microseconds of the call): the host's own figure,
+    /// under the HIP runtime the library links -- no other GPU runtime in the F# process.
+    member _.StepTimed(generations: int64) =
+        let mutable us = 0.0
+        check "gol_step_timed" (gol_step_timed(h, generations, &us)); us
     /// Wait for the board's work; reports a failed cooperative pass (GOL_ERR_HIP) like every readback.
     member _.Synchronize() = check "gol_synchronize" (gol_synchronize h)
     /// Path / tuning option (gol.h lists the names, e.g. "coop" 0); results are bit-identical for every setting.
     member this.SetOption(name: string, value: int64) =
         check "gol_set_option" (gol_set_option(h, name, value)); this
-    /// Halo transport of a multi-GPU board: 0 none (one part), 1 peer copies, 2 RCCL; with the reason.
+    /// Halo transport of a multi-GPU board: 0 none (one part), 1 peer copies (the default), 2 RCCL (after
+    /// SetOption("transport", 2L), one strip per GPU); with a description.
     member _.Transport() =
         let mutable t = 0
         let note = System.Text.StringBuilder(256)

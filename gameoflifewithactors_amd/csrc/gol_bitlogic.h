@@ -12,7 +12,7 @@
 //             (xor3 = LUT 0x96, majority = LUT 0xE8)
 //   vertical  t = sP + sC + sN + 2 (cP + cC + cN) is the 9-cell sum including the centre; the rule is
 //             next = (t == 3) | (alive & t == 4).  A = xor3(s), B = maj3(s), X = xor3(c), Y = maj3(c)
-//             then a 3-LUT tree found by exhaustive search (tests/test_bitlogic.py re-checks all 2^9
+//             then a 3-LUT tree found by exhaustive search (tests/cpp/test_bitlogic.cpp re-checks all 2^9
 //             neighbourhoods):  o1 = L(A, Y, alive; 0x27), o2 = L(B, X, Y; 0x19), next = L(o1, o2, A; 0x24).
 //
 // LUT convention used in this file: lut3(a, b, c, L) = bit (a | b<<1 | c<<2) of L.  gfx950's

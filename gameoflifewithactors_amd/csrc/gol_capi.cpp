@@ -161,7 +161,7 @@ constexpr int64_t kMidBoardCells = (int64_t)1 << 29;
 // W <= 128 and H <= 256, the reference's 100^2 board included) ran slower on it than on the per-generation
 // byte step in an interleaved A/B: 129x127 3.46 vs 3.10 us/generation, 200x100 3.65 vs 3.10, 181^2 6.26 vs
 // 3.15, 255x257 10.7 vs 3.1; only 255x64 was level, 3.00 vs 3.12 (profiles/r2/byte_cut_ab.log).
-// GOL_RESIDENT_MAX_CELLS still forces it (tests).
+// The board option "resident_max_cells" still forces it (tests).
 constexpr int64_t kResidentMaxCells = (int64_t)1 << 17;
 constexpr int64_t kResidentBytesMaxCells = 0;
 constexpr int64_t kResidentMaxGensPerLaunch = (int64_t)1 << 16;

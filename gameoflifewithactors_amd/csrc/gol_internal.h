@@ -45,7 +45,7 @@ int stream_largest_k(int64_t n, int cap, int ilv);
 int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0);
 int stream_pair_split(int k, int ilv, bool bounded);
 int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits = 0);
-// fills nstrips / nsegs / seg (one balanced round of resident waves unless GOL_SEG_ROWS is set)
+// fills nstrips / nsegs / seg (one balanced round of resident waves unless a.seg_opt -- the "seg_rows" option -- is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s);

@@ -8,8 +8,11 @@
 // (one 4*M-byte vector load per lane) is pushed through K generations held in registers -- per
 // generation level a 3-row window of horizontal row sums -- so a pass reads and writes the board once
 // per K generations.  Neighbour words come from the lane's own registers (interleaved layout), the
-// block-edge words from the neighbouring lanes (DPP wave_shr:1 / wave_shl:1), bit carries from
-// v_alignbit_b32, counts from v_bitop3_b32 (gol_bitlogic.h).  No LDS, no barriers, no atomics.
+// block-edge words from the neighbouring lanes (DPP wave_shr:1 / wave_shl:1, rotates on seam strips), bit carries
+// from v_alignbit_b32, counts from v_bitop3_b32 (gol_bitlogic.h).  No workgroup barriers and no atomics: each wave is
+// independent.  The deep passes (K > 1) stage the next trip's rows through the wave's own LDS slice
+// (buffer_load_dword ... lds, StreamWave::stage_load), which frees the prefetch registers; the K = 1 pass keeps a
+// second register buffer instead.
 //
 // Variants measured and removed from this file (DESIGN.md 4.1 "Negative results"; the logs stay under
 // profiles/r1/): full-row workgroups with an LDS edge exchange (fullrow_sweep.log), ds_bpermute cross-lane

@@ -6,8 +6,8 @@ pinned to the byte-per-cell oracle in tests/test_oracle.py) run on the same spli
 compared (canonical hash + population) with three GPU paths, each applying the rule of
 GameOfLifeLogic.fs:59-63 once per tick of GameOfLifeDriver.fs:32-40:
 
-  * the shipped single board (gol_create defaults: M = 2, K = 12 in 12-wave workgroups on a torus, K = 16
-    on a bounded board) -- the kernel bench.py times;
+  * the shipped single board (gol_create defaults: M = 2, K = 12 in 12-wave workgroups on both boundaries since
+    round 3; the bounded K = 16 pass keeps its own full-size case) -- the kernel bench.py times;
   * 8 ghost-row strips driven by one process (strips.LocalBoard): the per-rank kernel and halo geometry of
     the torchrun/RCCL bench path;
   * the one-handle multi-GPU board (gol_create_multi, 8 strips, peer-copied halos: csrc/gol_multi.cpp),

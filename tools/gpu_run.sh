@@ -1,6 +1,13 @@
 # GPU call script (gpurun): the current measurement call; each step under its own time limit, chained so that a failure ends the call
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3w; mkdir -p $O
-AB_PRE=300 timeout -k 10 500 bash tools/ab_rep.sh $O/ab_cutalign_torus.log 3 "2:12" gameoflifewithactors_amd/libgol_hip.so ab/lib_cutalign.so && grep -v amdgpu $O/ab_cutalign_torus.log | grep '^{' | cut -c1-160
-AB_BOUNDARY=1 AB_PRE=300 timeout -k 10 500 bash tools/ab_rep.sh $O/ab_cutalign_bounded.log 3 "2:12" gameoflifewithactors_amd/libgol_hip.so ab/lib_cutalign.so && grep -v amdgpu $O/ab_cutalign_bounded.log | grep '^{' | cut -c1-160
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4a; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -30 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_n1.log 2>&1 || { echo "bench rc=$?"; tail -5 $O/bench_n1.log; exit 1; }
+tail -c 1500 $O/bench_n1.log
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 > $O/bench_gloo2.log 2>&1 || { echo "gloo rc=$?"; tail -20 $O/bench_gloo2.log; exit 1; }
+tail -c 2500 $O/bench_gloo2.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_c2 -o c2 -- python3 $GRAFT_REPO_ROOT/bench.py --init dotnet-mod2 --seed 42 --width 4096 --height 4096 --generations 1000 --gens-per-step 1000 --steps 5 > $GRAFT_REPO_ROOT/$O/bench_c2.log 2>&1; echo "c2 profiled rc=$?"
+tail -c 1500 $GRAFT_REPO_ROOT/$O/bench_c2.log
