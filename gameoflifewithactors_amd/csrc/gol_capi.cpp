@@ -221,6 +221,8 @@ struct BoardOptions {
     int seam = 0;                             // "seam": torus seam strips (0 = where they apply, -1 = off)
     bool ragged_stream = true;                // "ragged_stream": ragged boards beyond the cooperative pass stream
                                               // packed words (0: the per-generation byte step)
+    bool ragged_ring = true;                  // "ragged_ring": ragged TORUS boards stream as ring rows on the aligned
+                                              // kernel (0: the M = 1 ragged-row variant with bit-level row ends)
     int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
@@ -236,6 +238,7 @@ struct gol_board {
     int64_t W = 0, H = 0;
     int boundary = GOL_TORUS;
     int tblock = 16;
+    bool tblock_set = false;  // tblock_k was given at creation (a cap), not the engine default
     bool packed = false;
     int ilv = 0;        // words per interleaved block (packed boards), 0 = byte board
     int64_t pitch = 0;  // words per row (packed)
@@ -250,10 +253,12 @@ struct gol_board {
     int64_t rag_words = 0;                  // capacity of each rag buffer
     // Ragged byte boards between gol_step calls of the multi-generation passes keep their state in the scratch rows:
     // 0 = the bytes (cells(cur)) are current; 1 = rag[rag_cur] holds it in the streaming pass's rows (rag_pitch words),
-    // 2 = in the cooperative pass's rows.  Every other access first brings the bytes up to date (sync_bytes).
+    // 2 = in the cooperative pass's rows, 3 = in ring rows (gol_formats.hip, layout rag_ilv).  Every other access first
+    // brings the bytes up to date (sync_bytes).
     int rag_state = 0;
     int rag_cur = 0;
     int64_t rag_pitch = 0;
+    int rag_ilv = 1;
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -340,7 +345,10 @@ int overwritten(gol_board* b) {
 // the bytes, on the board's stream, before anything reads or modifies them.
 int sync_bytes(gol_board* b) {
     if (!b->rag_state) return GOL_OK;
-    GOL_HIP(gol::launch_unpack_ragged(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_pitch, b->stream));
+    if (b->rag_state == 3)
+        GOL_HIP(gol::launch_unpack_ring(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_ilv, b->stream));
+    else
+        GOL_HIP(gol::launch_unpack_ragged(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_pitch, b->stream));
     b->rag_state = 0;
     return GOL_OK;
 }
@@ -544,6 +552,14 @@ bool use_stream_ragged(const gol_board* b) {
     return (b->W + 31) / 32 >= 64;  // rows of at least one wave strip (the strip geometry's assumption)
 }
 
+// Ragged torus boards on the streaming pass run as ring rows (gol_formats.hip): aligned rows of ring_pitch(W) words,
+// the board's cells at positions 64 .. 64 + W - 1 and copies of its ends around them, stepped by the ALIGNED torus
+// kernel (seam strips, interleaved blocks: the headline kernel's instruction stream) with the two copies rewritten
+// after every pass.  Layout and depth follow the aligned rules for a board of that many cells (board_ilv /
+// board_tblock): ilv 2 from 2^25 cells, K = 16 below 2^29 and 12 above.
+bool use_ring(const gol_board* b) { return b->boundary == GOL_TORUS && b->opt.ragged_ring; }
+int ring_ilv(const gol_board* b) { return gol::ring_pitch(b->W) * 32 * b->H < kSmallBoardCells ? 1 : 2; }
+
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
     if (gens <= 0) return GOL_OK;
@@ -554,7 +570,7 @@ int step_impl(gol_board* b, int64_t gens) {
     const int rag_next = wave ? 0
                               : (gens >= kCoopRaggedMinGens && use_coop_ragged(b, &rag_pitch)
                                      ? 2
-                                     : (gens >= kStreamRaggedMinGens && use_stream_ragged(b) ? 1 : 0));
+                                     : (gens >= kStreamRaggedMinGens && use_stream_ragged(b) ? (use_ring(b) ? 3 : 1) : 0));
     if (b->rag_state != rag_next)
         if (int rc = sync_bytes(b)) return rc;
     if (wave) {
@@ -586,6 +602,32 @@ int step_impl(gol_board* b, int64_t gens) {
         b->rag_pitch = rag_pitch;
         return rc;
     }
+    if (rag_next == 3) {
+        // the ragged torus board as ring rows (packed once, kept there after the call), the aligned streaming kernel
+        const int64_t pitch = gol::ring_pitch(b->W);
+        const int ilv = ring_ilv(b);
+        if (b->rag_state != 3) {
+            if (int rc = ensure_rag(b, pitch * b->H)) return rc;
+            GOL_HIP(gol::launch_pack_ring(b->cells(b->cur), b->rag[0], b->W, b->H, ilv, b->stream));
+            b->rag_cur = 0;
+        }
+        b->rag_state = 3;
+        b->rag_pitch = pitch;
+        b->rag_ilv = ilv;
+        while (gens > 0) {
+            const int k = gol::stream_largest_k(gens, b->tblock, ilv);
+            gol::StreamArgs a = b->stream_args(0, b->H, k);
+            a.words = pitch;
+            a.pitch = pitch;
+            a.ilv = ilv;
+            GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, false, true, b->stream));
+            GOL_HIP(gol::launch_ring_refresh(b->rag[b->rag_cur ^ 1], b->W, b->H, ilv, b->stream));
+            b->rag_cur ^= 1;
+            b->generation += k;
+            gens -= k;
+        }
+        return GOL_OK;
+    }
     if (rag_next == 1) {
         // the ragged byte board as whole words in scratch rows (packed once, kept there after the call), streaming
         const int64_t nw = (b->W + 31) / 32;
@@ -596,8 +638,10 @@ int step_impl(gol_board* b, int64_t gens) {
         }
         b->rag_state = 1;
         b->rag_pitch = nw;
+        // a torus board's default depth is the ring rows' (create_impl); this M = 1 path keeps its own
+        const int cap = b->tblock_set || b->boundary != GOL_TORUS ? b->tblock : board_tblock(0, b->W * b->H, GOL_TORUS);
         while (gens > 0) {
-            const int k = gol::stream_largest_k(gens, b->tblock, 1);
+            const int k = gol::stream_largest_k(gens, cap, 1);
             gol::StreamArgs a = b->stream_args(0, b->H, k);
             a.words = nw;
             a.pitch = nw;
@@ -838,6 +882,12 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n)) : 0;
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
+        if (!b->packed && boundary == GOL_TORUS && !tblock_k) {
+            // ragged torus boards stream as ring rows of ring_pitch(W) words: the aligned rules for that many cells
+            const int64_t ring_cells = gol::ring_pitch(width) * 32 * height;
+            b->tblock = board_tblock(ring_cells < kSmallBoardCells ? 1 : 2, ring_cells, boundary);
+        }
+        b->tblock_set = tblock_k != 0;
         b->pitch = b->packed ? width / 32 : 0;
         hipError_t e = devices ? hipSetDevice(devices[0]) : hipSuccess;
         if (e == hipSuccess) e = hipGetDevice(&b->device);
@@ -1295,6 +1345,7 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         return b->multi->set_transport((int)value);
     }
     else if (n == "ragged_stream") o.ragged_stream = value != 0;
+    else if (n == "ragged_ring") o.ragged_ring = value != 0;
     else if (n == "coop_r") {
         if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
         o.coop_r = (int)value;
@@ -1332,6 +1383,7 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "seg_rows") *value = o.seg_rows;
     else if (n == "seam") *value = o.seam;
     else if (n == "ragged_stream") *value = o.ragged_stream;
+    else if (n == "ragged_ring") *value = o.ragged_ring;
     else if (n == "coop_r") *value = o.coop_r;
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
     else if (n == "coop_spin_limit") *value = o.coop_spin_limit;

@@ -112,6 +112,106 @@ __global__ __launch_bounds__(256) void gol_unpack_ragged(const uint32_t* __restr
     }
 }
 
+// ---- Ring rows of a ragged TORUS board (DESIGN.md 4.1 "Ragged rows: ring rows").  A row of W cells (W not a multiple
+// of 32) is a ring (GameOfLifeDriver.fs:21-25).  It is stored as an ALIGNED row of Wp = 64 * ceil((W + 2 * 64) / 64)
+// cells in the packed layout `ilv` (1 or 2): ring position u holds cell x = (u - 64) mod W, so u in [64, 64 + W) are
+// the board's cells, u in [0, 64) a copy of its last 64 cells and u in [64 + W, Wp) a copy of its first Wp - W - 64
+// (>= 64).  The aligned streaming kernel then steps the ring rows as a torus of width Wp: the only wrong neighbours
+// are at the two ends of the extended row, and after a pass of k <= 64 generations their errors have spread k cells,
+// not into the board's cells; gol_ring_refresh then rewrites both copies from the board's cells.  Blocks of 64
+// cells: u-block c holds words 2c, 2c + 1 (ilv 2: even / odd cells; ilv 1: cells 0-31 / 32-63 of the block).
+constexpr int64_t kRingPad = 64;  // ring positions before the board's first cell
+
+__device__ __forceinline__ uint32_t even_bits64(uint64_t x) {
+    x &= 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+    return (uint32_t)x;
+}
+// word p (0 / 1) of a 64-cell block given as a mask (bit i = cell i of the block)
+__device__ __forceinline__ uint32_t ring_word(uint64_t m, int p, int ilv) {
+    return ilv == 2 ? even_bits64(m >> p) : (uint32_t)(m >> (32 * p));
+}
+// bit of ring position u of a row
+__device__ __forceinline__ uint32_t ring_bit(const uint32_t* row, int64_t u, int ilv) {
+    const int64_t c = u >> 6;
+    const int i = (int)(u & 63);
+    const int64_t w = 2 * c + (ilv == 2 ? (i & 1) : (i >> 5));
+    return (row[w] >> (ilv == 2 ? (i >> 1) : (i & 31))) & 1u;
+}
+
+// bytes -> ring rows.  One wavefront per chunk of 32 u-blocks (64 words) of a row: 64 consecutive ring positions per
+// wave load (coalesced except at the two wraps), ballot per block, lanes 2i / 2i + 1 keep block i's words.
+__global__ __launch_bounds__(256) void gol_pack_ring(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words,
+                                                     int64_t W, int64_t H, int64_t pitch, int ilv) {
+    int64_t y, w0;
+    if (!ragged_chunk(pitch, H, y, w0)) return;
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t row =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cells + y * W), (short)0, (int)W, 0x00020000);
+    const int64_t Wp = pitch * 32;
+    uint8_t v[kChunkWords / 2];
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++) {
+        const int64_t u = (w0 + 2 * i) * 32 + lane;
+        int64_t x = u - kRingPad;
+        x = x < 0 ? x + W : (x >= W ? x - W : x);
+        v[i] = __builtin_amdgcn_raw_buffer_load_b8(row, u < Wp ? (int)x : (int)W, 0, 0);  // past the row: 0
+    }
+    uint64_t mine = 0;  // the block of word w0 + lane
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++) {
+        const uint64_t m = __ballot(v[i] != 0);
+        mine = (lane >> 1) == i ? m : mine;
+    }
+    if (w0 + lane < pitch) words[y * pitch + w0 + lane] = ring_word(mine, lane & 1, ilv);
+}
+
+// ring rows -> bytes (the board's W cells as 0 / 1).  One wavefront per chunk of 32 x-blocks: x-block c is u-block
+// c + 1 (kRingPad = 64), whose two words lanes 2i / 2i + 1 load; lane l stores cell 64 c + l.
+__global__ __launch_bounds__(256) void gol_unpack_ring(const uint32_t* __restrict__ words, uint8_t* __restrict__ cells,
+                                                       int64_t W, int64_t H, int64_t pitch, int ilv) {
+    const int64_t nxw = 2 * ((W + 63) / 64);  // words covering the board's cells
+    int64_t y, w0;
+    if (!ragged_chunk(nxw, H, y, w0)) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wi = 2 + w0 + lane;
+    const uint32_t mine = w0 + lane < nxw && wi < pitch ? words[y * pitch + wi] : 0u;
+    const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(cells + y * W, (short)0, (int)W, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kChunkWords / 2; i++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * i);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)mine, 2 * i + 1);
+        const uint32_t bit = ilv == 2 ? (((lane & 1) ? hi : lo) >> (lane >> 1)) & 1u
+                                      : ((lane < 32 ? lo : hi) >> (lane & 31)) & 1u;
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bit, row, (int)((w0 + 2 * i) * 32) + lane, 0, 0);
+    }
+}
+
+// After a pass: rewrite the copies at both ends of every ring row from the board's cells (u-block 0 <- positions
+// u + W; positions u >= 64 + W <- u - W; the board's own cells in the first suffix block are kept).  One wavefront per
+// row; every source position lies in [64, 64 + W), which this kernel never writes.
+__global__ __launch_bounds__(256) void gol_ring_refresh(uint32_t* __restrict__ words, int64_t W, int64_t H,
+                                                        int64_t pitch, int ilv) {
+    const int64_t y = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (y >= H) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t* row = words + y * pitch;
+    const int64_t nblk = pitch / 2, end = kRingPad + W;
+    const int64_t first_suffix = end >> 6;
+    for (int64_t c = -1; c < nblk; c = c < 0 ? first_suffix : c + 1) {
+        const int64_t cb = c < 0 ? 0 : c;
+        const int64_t u = cb * 64 + lane;
+        const int64_t src = c < 0 ? u + W : (u >= end ? u - W : u);
+        const uint64_t m = __ballot(ring_bit(row, src, ilv) != 0);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 2) row[2 * cb + lane] = ring_word(m, lane, ilv);
+    }
+}
+
 // packed -> bytes: out[x + y*stride] = alive ? value : 0; one thread per stored word
 __global__ void gol_unpack(const uint32_t* __restrict__ words, uint8_t* __restrict__ out, int64_t W, int64_t rows,
                            int64_t pitch, int64_t row0, int64_t stride, uint8_t value, int ilv) {
@@ -364,6 +464,31 @@ hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W
     if (pitch < (W + 31) / 32 || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gol_unpack_ragged, dim3(ragged_blocks((W + 31) / 32, H)), dim3(256), 0, s, words, cells, W, H,
                        pitch);
+    return hipGetLastError();
+}
+
+int64_t ring_pitch(int64_t W) { return 2 * ((W + 2 * kRingPad + 63) / 64); }
+
+hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s) {
+    const int64_t pitch = ring_pitch(W);
+    if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gol_pack_ring, dim3(ragged_blocks(pitch, H)), dim3(256), 0, s, cells, words, W, H, pitch, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, hipStream_t s) {
+    const int64_t pitch = ring_pitch(W);
+    if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gol_unpack_ring, dim3(ragged_blocks(2 * ((W + 63) / 64), H)), dim3(256), 0, s, words, cells, W,
+                       H, pitch, ilv);
+    return hipGetLastError();
+}
+
+hipError_t launch_ring_refresh(uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s) {
+    if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gol_ring_refresh, dim3((unsigned)((H + 3) / 4)), dim3(256), 0, s, words, W, H, ring_pitch(W), ilv);
     return hipGetLastError();
 }
 

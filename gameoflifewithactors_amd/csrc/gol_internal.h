@@ -61,6 +61,12 @@ hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W
                                 hipStream_t s);
 hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                          int64_t stride, uint8_t value, int ilv, hipStream_t s);
+// Ring rows of a ragged torus board (gol_formats.hip): an aligned row of ring_pitch(W) words in layout ilv (1 or 2),
+// position u = cell (u - 64) mod W; pack / unpack against the byte board and the per-pass refresh of the two copies
+int64_t ring_pitch(int64_t W);
+hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s);
+hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, hipStream_t s);
+hipError_t launch_ring_refresh(uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s);
 hipError_t launch_region(const void* board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
                          int64_t h, uint8_t* out, hipStream_t s);
 hipError_t launch_bytes_render(const uint8_t* cells, uint8_t* out, int64_t W, int64_t H, int64_t stride,

@@ -1,5 +1,6 @@
-"""GPU parity of ragged boards on the streaming pass (csrc/gol_step.hip kRagged / the column-masked bounded
-variant; DESIGN.md 4.1 "Ragged rows").
+"""GPU parity of ragged boards on the streaming pass (torus: ring rows on the aligned kernel, gol_formats.hip
+gol_pack_ring / gol_ring_refresh, or with the board option "ragged_ring" 0 the M = 1 kRagged variant of
+csrc/gol_step.hip; bounded: the column-masked variant; DESIGN.md 4.1 "Ragged rows").
 
 The reference's board size is any integer (GameOfLifeLogic.fs:5, GameofLife.fs:18).  Byte boards whose width is not
 a multiple of 32 and that the cooperative pass does not take (wider than 8192 cells or above 2^26 cells) run the
@@ -27,9 +28,9 @@ def _rand(h, w, seed, p=0.4):
     return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
 
 
-def _run(gol, b0, boundary, steps, stream, tblock_k=0):
+def _run(gol, b0, boundary, steps, stream, tblock_k=0, ring=1):
     h, w = b0.shape
-    with gol.Board(w, h, boundary, tblock_k=tblock_k, options={"ragged_stream": int(stream)}) as b:
+    with gol.Board(w, h, boundary, tblock_k=tblock_k, options={"ragged_stream": int(stream), "ragged_ring": ring}) as b:
         assert not b.info()["packed"]
         b.set_cells(b0)
         for g in steps:
@@ -43,14 +44,36 @@ def _run(gol, b0, boundary, steps, stream, tblock_k=0):
 WIDTHS = [8193, 8209, 8223, 10001, 62 * 133 * 32 - 31, 62 * 134 * 32 + 5, 16383]
 
 
-@pytest.mark.parametrize("boundary", [0, 1])
+@pytest.mark.parametrize("boundary,ring", [(0, 1), (0, 0), (1, 1)])
 @pytest.mark.parametrize("w", WIDTHS)
-def test_ragged_stream_matches_oracle(gol, oracle, w, boundary):
+def test_ragged_stream_matches_oracle(gol, oracle, w, boundary, ring):
     h = 70
     b0 = _rand(h, w, w + boundary)
     steps = [21, 3, 16]  # 16 + 4 + 1, the byte step for the 3-generation call, 16
     want = oracle.c_run(b0, sum(steps), boundary)
-    np.testing.assert_array_equal(_run(gol, b0, boundary, steps, stream=True), want)
+    np.testing.assert_array_equal(_run(gol, b0, boundary, steps, stream=True, ring=ring), want)
+
+
+# ring rows at ilv 2 (above 2^25 ring cells): the widths' last 64-cell block holds 1 .. 63 of the board's cells, the
+# seam geometry (>= 63 blocks) and not
+@pytest.mark.parametrize("w", [8193, 8255, 10001, 16383, 16447, 4033 * 8 + 1])
+def test_ragged_ring_interleaved(gol, oracle, w):
+    h = (1 << 25) // w + 40
+    b0 = _rand(h, w, w, p=0.3)
+    with gol.Board(w, h, 0, options={"coop": 0}) as b:
+        assert b.info()["tblock_k"] == 16
+        b.set_cells(b0).step(16 + 12 + 5)
+        got_rows = b.get_region(0, 0, w, 64)
+        got_end = b.get_region(0, h - 40, w, 40)
+        b.set_option("ragged_ring", 0)
+        b.set_cells(b0).step(16 + 12 + 5)
+        np.testing.assert_array_equal(b.get_region(0, 0, w, 64), got_rows)
+        np.testing.assert_array_equal(b.get_region(0, h - 40, w, 40), got_end)
+    # the first 64 rows against the oracle's light cone (the torus rows wrap: rows h-33 .. h-1 above row 0)
+    gens = 33
+    win = np.concatenate([b0[h - gens:], b0[:64 + gens]], axis=0)
+    sub = oracle.c_run(np.ascontiguousarray(win), gens, 0)  # the window's own y wrap only pollutes the cone edges
+    np.testing.assert_array_equal(got_rows, sub[gens:gens + 64])
 
 
 @pytest.mark.parametrize("k", [1, 2, 8, 16, 24, 32])
