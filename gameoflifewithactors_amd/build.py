@@ -51,9 +51,13 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines: tu
         return lib
     objs = []
     tag = "_".join(d.replace("=", "") for d in defines) + ("_alt" if step_src or alt else "") + ("_fl" if flags else "")
+    # A/B variants' objects and libraries stay under build/ (git-ignored), not beside the shipped sources
+    objdir = os.path.join(ROOT, "build", "obj") if tag else CSRC
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
     procs = []
     for src in sources:  # compile the translation units in parallel (gol_step.hip dominates)
-        obj = os.path.join(CSRC, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")
+        obj = os.path.join(objdir, os.path.basename(src) + (f".{tag}" if tag else "") + ".o")
         cmd = [
             _hipcc(),
             f"--offload-arch={ARCH}",

@@ -206,6 +206,15 @@ struct StreamWave {
 #define GOL_AB_NOSEAM 0
 #endif
     static constexpr bool kSeam = !GOL_AB_NOSEAM && !BOUNDED && !(K == 1) && !kRagged;
+    // ONE seam DMA per trip (round 4): a global_load_lds_dword with a per-lane address, lane i loading word i % M of
+    // the block left of lane 0 in row (i / M) % R of the trip; the R x M words land side by side in a 64-dword LDS
+    // slot, which every lane then reads as a broadcast and only the seam lane merges (`hmask`).  Round 3 issued M
+    // DMAs per row (every lane reloading its own word, a cache hit, so that one lane in 64 got its half-block): twice
+    // the bounded pass's VMEM and LDS instructions (SQ_INSTS_VMEM_RD / SQ_INSTS_LDS 1.93x, profiles/r3/pmc_sq).
+#ifndef GOL_SEAM1
+#define GOL_SEAM1 1
+#endif
+    static constexpr bool kSeam1 = kSeam && GOL_SEAM1;
     // Deep passes (K > 1) stage their prefetched rows through LDS (see `stage` below); the K = 1 pass keeps two
     // register buffers (it has registers to spare, and its halo-free strips load a neighbour word per row).
     static constexpr bool kStage = !kNoHalo;
@@ -230,8 +239,15 @@ struct StreamWave {
     // than the (12, 2) pass has, and it spilled.)
     static constexpr int kDmaWords = 1;  // dwords per lane per DMA
     static constexpr int kDmas = M;      // DMAs per row and kind
-    using Stage = uint32_t[2][kSeam ? 2 : 1][R][kDmas][kWave * kDmaWords];  // [parity][row, seam][row][dma][lane x words]
+    using Stage = uint32_t[2][kSeam && !kSeam1 ? 2 : 1][R][kDmas][kWave * kDmaWords];  // [parity][row, seam][row][dma][lane x words]
     Stage* stage = nullptr;
+    // kSeam1: the per-trip seam slot [parity][lane], this lane's row (relative to the trip's first) and byte offset in
+    // the seam DMA, and the seam lane's merge mask (0xffff0000 on the seam lane of a seam strip, 0 elsewhere: remainder
+    // waves and halo-lane strips merge nothing)
+    using SeamStage = uint32_t[2][kWave];
+    SeamStage* seam1 = nullptr;
+    int seam1_delta = 0;  // (lane / M) % R rows + the word (lane % M) of the block left of lane 0, in bytes
+    uint32_t hmask = 0;
     template <int WORDS>
     __device__ __forceinline__ static void dma(__amdgpu_buffer_rsrc_t rs, uint32_t* lds, int off) {
         auto* p = (__attribute__((address_space(3))) void*)lds;
@@ -376,6 +392,11 @@ struct StreamWave {
                 span_bytes = (int64_t)(rem_count - 1) * a.seg * a.pitch * 4 + row_bytes;
             }
             if (lane < kSeamInterior || !a.seam || rem_count) seam_off = load_off;
+            if constexpr (kSeam1) {
+                seam1_delta = (int)(((lane / M) % R) * a.pitch * 4) + 4 * (lane % M) +
+                              (a.seam && rem_count == 0 ? (int)(floor_mod(sx * kSeamInterior - 1, nblocks) * 4 * M) : 0);
+                hmask = a.seam && rem_count == 0 && lane == kWave - 1 ? 0xffff0000u : 0u;
+            }
         }
         seg_begin = a.out_begin + sy * a.seg;
         seg_end = seg_begin + a.seg < a.out_end ? seg_begin + a.seg : a.out_end;
@@ -486,12 +507,37 @@ struct StreamWave {
     // KINDS: 1 = the row's own-word DMAs (advancing the row walk; the descriptor is kept for the seam DMAs), 2 = its
     // seam DMAs (kept descriptor), 3 = both
     __amdgpu_buffer_rsrc_t row_rs[R];
+    // kSeam1: the trip's one seam DMA, issued with its first row (buffer row br0, wave-uniform): lane i loads from row
+    // br0 + (i / M) % R through a range-checked descriptor based at row br0.  Ghost-row strips: rows past the buffer
+    // (only the tail trip's unused rows) read as 0.  Single board: a trip whose rows wrap past the board's last row
+    // (first and last segments) splits the lanes -- rows before the wrap from the descriptor at br0, the others from
+    // one based at row 0 -- so every lane reads its row.  No per-lane 64-bit address is formed.
+    template <int PAR>
+    __device__ __forceinline__ void stage_load_seam1(int64_t br0) {
+        const int64_t pb = a.pitch * 4;
+        uint32_t* lds = &(*seam1)[PAR][0];
+        const uint32_t* base = src + br0 * a.pitch;
+        if (WRAP_ROWS) {
+            if (br0 + R <= a.rows) {
+                dma<1>(row_rsrc(base, R * pb), lds, seam1_delta);
+            } else {
+                const int n1 = (int)((a.rows - br0) * pb);  // bytes of the rows before the wrap (>= one row)
+                if (seam1_delta < n1)
+                    dma<1>(row_rsrc(base, n1), lds, seam1_delta);
+                else
+                    dma<1>(row_rsrc(src, R * pb), lds, seam1_delta - n1);
+            }
+        } else {
+            const int64_t left = (a.rows + 2 * a.ghost - br0) * pb;
+            dma<1>(row_rsrc(base, left < R * pb ? left : R * pb), lds, seam1_delta);
+        }
+    }
     template <int PAR, int KINDS>
     __device__ __forceinline__ void stage_load_row(int r) {
         if constexpr ((KINDS & 1) == 0) {
 #pragma unroll
             for (int d = 0; d < kDmas; d++)
-                if constexpr (kSeam) dma<kDmaWords>(row_rs[r], &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
+                if constexpr (kSeam && !kSeam1) dma<kDmaWords>(row_rs[r], &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
         } else {
             __amdgpu_buffer_rsrc_t rs;
             if constexpr (BOUNDED) {
@@ -510,12 +556,15 @@ struct StreamWave {
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
                 rs = row_rsrc(src + br * a.pitch, span_bytes);
+                if constexpr (kSeam1)
+                    if (r == 0) stage_load_seam1<PAR>(br);
             }
-            if constexpr ((KINDS & 2) == 0) row_rs[r] = rs;
+            if constexpr ((KINDS & 2) == 0 && !kSeam1) row_rs[r] = rs;
 #pragma unroll
             for (int d = 0; d < kDmas; d++) {
                 dma<kDmaWords>(rs, &(*stage)[PAR][0][r][d][0], load_off + 4 * d);
-                if constexpr (kSeam && (KINDS & 2)) dma<kDmaWords>(rs, &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
+                if constexpr (kSeam && !kSeam1 && (KINDS & 2))
+                    dma<kDmaWords>(rs, &(*stage)[PAR][kSeam ? 1 : 0][r][d][0], seam_off + 4 * d);
             }
         }
     }
@@ -549,7 +598,12 @@ struct StreamWave {
     }
     template <int PAR>
     __device__ __forceinline__ void stage_read_seam(Seam& t, int lane) {
-        if constexpr (kSeam) {
+        if constexpr (kSeam1) {  // the same R x M words for every lane (a broadcast read)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int j = 0; j < M; j++) t.s[r][j] = (*seam1)[PAR][r * M + j];
+        } else if constexpr (kSeam) {
 #pragma unroll
             for (int r = 0; r < R; r++)
 #pragma unroll
@@ -567,7 +621,9 @@ struct StreamWave {
             if constexpr (BOUNDED) rm = row_mask((int)first_step + r);
 #pragma unroll
             for (int j = 0; j < M; j++) {
-                if constexpr (kSeam)
+                if constexpr (kSeam1)
+                    v[r][j] = lut3<0xD8>(hmask, t.s[kSeam ? r : 0][j], v[r][j]);
+                else if constexpr (kSeam)
                     v[r][j] = lut3<0xD8>(0xffff0000u, t.s[kSeam ? r : 0][j], v[r][j]);
                 else if constexpr (BOUNDED)
                     v[r][j] = kColMask ? lut3<0x80>(v[r][j], colmask, rm) : v[r][j] & rm;
@@ -783,6 +839,8 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
         // trip earlier (the wait-count pass treats pending loads and stores as completing out of order).
         __shared__ typename W::Stage stage[WPB];
         w.stage = &stage[wave];
+        __shared__ uint32_t seam1_stage[W::kSeam1 ? WPB : 1][2][W::kSeam1 ? kWave : 1];
+        if constexpr (W::kSeam1) w.seam1 = &seam1_stage[wave];
         uint32_t NV[R];  // (K = 1 neighbour words: unused here)
 #pragma unroll
         for (int r = 0; r < R; r++) NV[r] = 0;

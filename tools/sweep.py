@@ -1,7 +1,7 @@
 """Sweep temporal-block depth k (and optionally segment rows) on one GPU; prints one JSON line per config.
 
     python tools/sweep.py --size 65536 --ks 1,2,4,8,16,24,32 --passes 8
-Timing: HIP events on the board's own stream around `passes` launches (after 2 warm-up launches).
+Timing: the library's own HIP events around `passes` launches (gol_step_timed, after 2 warm-up launches); no torch.
 """
 import argparse
 import json
@@ -25,8 +25,6 @@ def main():
     p.add_argument("--pre", type=int, default=0, help="generations stepped before the timed passes (bench.py's window "
                    "starts at generation 312)")
     a = p.parse_args()
-    import torch
-
     from gameoflifewithactors_amd import Board, _lib
 
     W = a.size
@@ -41,18 +39,13 @@ def main():
             continue
         with Board(W, H, a.boundary, tblock_k=k, ilv=ilv, options=opts) as b:
             b.seed_splitmix(0x5EED)
-            s = torch.cuda.ExternalStream(b.stream)
             b.step(2 * k + a.pre)
             b.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            b.step(a.passes * k)
-            e1.record(s)
-            b.synchronize()
-            t = e0.elapsed_time(e1) / 1e3 / a.passes
+            t = b.step_timed(a.passes * k) / 1e6 / a.passes
+            h = b.hash()
             gcups = W * H * k / t / 1e9
             print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "split": a.split, "pre": a.pre, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
-                              "alg_GBps": round(W * H / 4 / t / 1e9, 1),
+                              "alg_GBps": round(W * H / 4 / t / 1e9, 1), "hash": f"{h:016x}",
                               }), flush=True)
 
 
