@@ -221,8 +221,9 @@ struct BoardOptions {
     int seam = 0;                             // "seam": torus seam strips (0 = where they apply, -1 = off)
     bool ragged_stream = true;                // "ragged_stream": ragged boards beyond the cooperative pass stream
                                               // packed words (0: the per-generation byte step)
-    bool ragged_ring = true;                  // "ragged_ring": ragged TORUS boards stream as ring rows on the aligned
-                                              // kernel (0: the M = 1 ragged-row variant with bit-level row ends)
+    bool ragged_ring = true;                  // "ragged_ring": ragged boards stream as block rows (torus: ring rows on
+                                              // the aligned kernel; bounded: column-masked block rows) in the aligned
+                                              // layouts (0: ilv-1 rows, bit-level row ends on a torus)
     int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
@@ -346,7 +347,8 @@ int overwritten(gol_board* b) {
 int sync_bytes(gol_board* b) {
     if (!b->rag_state) return GOL_OK;
     if (b->rag_state == 3)
-        GOL_HIP(gol::launch_unpack_ring(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_ilv, b->stream));
+        GOL_HIP(gol::launch_unpack_ring(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_ilv,
+                                        b->boundary == GOL_TORUS, b->stream));
     else
         GOL_HIP(gol::launch_unpack_ragged(b->rag[b->rag_cur], b->cells(b->cur), b->W, b->H, b->rag_pitch, b->stream));
     b->rag_state = 0;
@@ -552,13 +554,15 @@ bool use_stream_ragged(const gol_board* b) {
     return (b->W + 31) / 32 >= 64;  // rows of at least one wave strip (the strip geometry's assumption)
 }
 
-// Ragged torus boards on the streaming pass run as ring rows (gol_formats.hip): aligned rows of ring_pitch(W) words,
-// the board's cells at positions 64 .. 64 + W - 1 and copies of its ends around them, stepped by the ALIGNED torus
-// kernel (seam strips, interleaved blocks: the headline kernel's instruction stream) with the two copies rewritten
-// after every pass.  Layout and depth follow the aligned rules for a board of that many cells (board_ilv /
-// board_tblock): ilv 2 from 2^25 cells, K = 16 below 2^29 and 12 above.
-bool use_ring(const gol_board* b) { return b->boundary == GOL_TORUS && b->opt.ragged_ring; }
-int ring_ilv(const gol_board* b) { return gol::ring_pitch(b->W) * 32 * b->H < kSmallBoardCells ? 1 : 2; }
+// Ragged boards on the streaming pass run as block rows (gol_formats.hip) in the aligned layouts.  Torus: ring rows
+// of ring_pitch(W) words, the board's cells at positions 64 .. 64 + W - 1 and copies of its ends around them, stepped
+// by the ALIGNED torus kernel (seam strips, interleaved blocks: the headline kernel's instruction stream) with the two
+// copies rewritten after every pass.  Bounded: rows of ceil(W / 64) blocks, the last one partial, on edge-fill strips
+// that AND per-word column masks at every level (gol_step.hip NARROW = 2).  Layout and depth follow the aligned rules
+// for a board of that many cells (board_ilv / board_tblock): ilv 2 from 2^25 cells, K = 16 below 2^29, 12 above.
+bool use_ring(const gol_board* b) { return b->opt.ragged_ring; }
+int64_t ring_cells(int64_t W, int64_t H, int boundary) { return gol::ring_pitch(W, boundary == GOL_TORUS) * 32 * H; }
+int ring_ilv(const gol_board* b) { return ring_cells(b->W, b->H, b->boundary) < kSmallBoardCells ? 1 : 2; }
 
 int step_impl(gol_board* b, int64_t gens) {
     if (b->multi) return b->multi->step(gens, &b->generation);
@@ -603,12 +607,13 @@ int step_impl(gol_board* b, int64_t gens) {
         return rc;
     }
     if (rag_next == 3) {
-        // the ragged torus board as ring rows (packed once, kept there after the call), the aligned streaming kernel
-        const int64_t pitch = gol::ring_pitch(b->W);
+        // the ragged board as block rows (packed once, kept there after the call), the aligned streaming kernel
+        const bool torus = b->boundary == GOL_TORUS;
+        const int64_t pitch = gol::ring_pitch(b->W, torus);
         const int ilv = ring_ilv(b);
         if (b->rag_state != 3) {
             if (int rc = ensure_rag(b, pitch * b->H)) return rc;
-            GOL_HIP(gol::launch_pack_ring(b->cells(b->cur), b->rag[0], b->W, b->H, ilv, b->stream));
+            GOL_HIP(gol::launch_pack_ring(b->cells(b->cur), b->rag[0], b->W, b->H, ilv, torus, b->stream));
             b->rag_cur = 0;
         }
         b->rag_state = 3;
@@ -620,8 +625,12 @@ int step_impl(gol_board* b, int64_t gens) {
             a.words = pitch;
             a.pitch = pitch;
             a.ilv = ilv;
-            GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, false, true, b->stream));
-            GOL_HIP(gol::launch_ring_refresh(b->rag[b->rag_cur ^ 1], b->W, b->H, ilv, b->stream));
+            if (!torus) {  // cells past the row's end stay dead (column masks)
+                a.rag_bits = (int32_t)(b->W % 32);
+                a.rag_w = b->W;
+            }
+            GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, !torus, torus, b->stream));
+            if (torus) GOL_HIP(gol::launch_ring_refresh(b->rag[b->rag_cur ^ 1], b->W, b->H, ilv, b->stream));
             b->rag_cur ^= 1;
             b->generation += k;
             gens -= k;
@@ -638,8 +647,8 @@ int step_impl(gol_board* b, int64_t gens) {
         }
         b->rag_state = 1;
         b->rag_pitch = nw;
-        // a torus board's default depth is the ring rows' (create_impl); this M = 1 path keeps its own
-        const int cap = b->tblock_set || b->boundary != GOL_TORUS ? b->tblock : board_tblock(0, b->W * b->H, GOL_TORUS);
+        // a ragged board's default depth is the block rows' (create_impl); this M = 1 path keeps its own
+        const int cap = b->tblock_set ? b->tblock : board_tblock(0, b->W * b->H, b->boundary);
         while (gens > 0) {
             const int k = gol::stream_largest_k(gens, cap, 1);
             gol::StreamArgs a = b->stream_args(0, b->H, k);
@@ -647,6 +656,7 @@ int step_impl(gol_board* b, int64_t gens) {
             a.pitch = nw;
             a.ilv = 1;
             a.rag_bits = (int32_t)(b->W % 32);
+            a.rag_w = b->boundary == GOL_BOUNDED ? b->W : 0;
             GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, b->boundary == GOL_BOUNDED,
                                             b->boundary == GOL_TORUS, b->stream));
             b->rag_cur ^= 1;
@@ -882,10 +892,10 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n)) : 0;
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
-        if (!b->packed && boundary == GOL_TORUS && !tblock_k) {
-            // ragged torus boards stream as ring rows of ring_pitch(W) words: the aligned rules for that many cells
-            const int64_t ring_cells = gol::ring_pitch(width) * 32 * height;
-            b->tblock = board_tblock(ring_cells < kSmallBoardCells ? 1 : 2, ring_cells, boundary);
+        if (!b->packed && !tblock_k) {
+            // ragged boards stream as block rows of ring_pitch(W) words: the aligned rules for that many cells
+            const int64_t rc = ring_cells(width, height, boundary);
+            b->tblock = board_tblock(rc < kSmallBoardCells ? 1 : 2, rc, boundary);
         }
         b->tblock_set = tblock_k != 0;
         b->pitch = b->packed ? width / 32 : 0;

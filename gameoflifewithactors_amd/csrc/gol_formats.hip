@@ -120,7 +120,9 @@ __global__ __launch_bounds__(256) void gol_unpack_ragged(const uint32_t* __restr
 // are at the two ends of the extended row, and after a pass of k <= 64 generations their errors have spread k cells,
 // not into the board's cells; gol_ring_refresh then rewrites both copies from the board's cells.  Blocks of 64
 // cells: u-block c holds words 2c, 2c + 1 (ilv 2: even / odd cells; ilv 1: cells 0-31 / 32-63 of the block).
-constexpr int64_t kRingPad = 64;  // ring positions before the board's first cell
+// A ragged BOUNDED board uses the same block rows without the copies (pad 0: position u = cell u, cells past W zero,
+// ceil(W / 64) blocks per row); the kernel's column masks keep those cells dead (gol_step.hip NARROW = 2).
+constexpr int64_t kRingPad = 64;  // ring positions before the board's first cell (torus)
 
 __device__ __forceinline__ uint32_t even_bits64(uint64_t x) {
     x &= 0x5555555555555555ull;
@@ -146,7 +148,7 @@ __device__ __forceinline__ uint32_t ring_bit(const uint32_t* row, int64_t u, int
 // bytes -> ring rows.  One wavefront per chunk of 32 u-blocks (64 words) of a row: 64 consecutive ring positions per
 // wave load (coalesced except at the two wraps), ballot per block, lanes 2i / 2i + 1 keep block i's words.
 __global__ __launch_bounds__(256) void gol_pack_ring(const uint8_t* __restrict__ cells, uint32_t* __restrict__ words,
-                                                     int64_t W, int64_t H, int64_t pitch, int ilv) {
+                                                     int64_t W, int64_t H, int64_t pitch, int ilv, int64_t pad) {
     int64_t y, w0;
     if (!ragged_chunk(pitch, H, y, w0)) return;
     const int lane = threadIdx.x & 63;
@@ -157,9 +159,9 @@ __global__ __launch_bounds__(256) void gol_pack_ring(const uint8_t* __restrict__
 #pragma unroll
     for (int i = 0; i < kChunkWords / 2; i++) {
         const int64_t u = (w0 + 2 * i) * 32 + lane;
-        int64_t x = u - kRingPad;
-        x = x < 0 ? x + W : (x >= W ? x - W : x);
-        v[i] = __builtin_amdgcn_raw_buffer_load_b8(row, u < Wp ? (int)x : (int)W, 0, 0);  // past the row: 0
+        int64_t x = u - pad;
+        if (pad) x = x < 0 ? x + W : (x >= W ? x - W : x);  // the ring's copies (pad 0: cells past W read as 0)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b8(row, u < Wp && x < W ? (int)x : (int)W, 0, 0);  // past the row: 0
     }
     uint64_t mine = 0;  // the block of word w0 + lane
 #pragma unroll
@@ -173,12 +175,12 @@ __global__ __launch_bounds__(256) void gol_pack_ring(const uint8_t* __restrict__
 // ring rows -> bytes (the board's W cells as 0 / 1).  One wavefront per chunk of 32 x-blocks: x-block c is u-block
 // c + 1 (kRingPad = 64), whose two words lanes 2i / 2i + 1 load; lane l stores cell 64 c + l.
 __global__ __launch_bounds__(256) void gol_unpack_ring(const uint32_t* __restrict__ words, uint8_t* __restrict__ cells,
-                                                       int64_t W, int64_t H, int64_t pitch, int ilv) {
+                                                       int64_t W, int64_t H, int64_t pitch, int ilv, int64_t pad) {
     const int64_t nxw = 2 * ((W + 63) / 64);  // words covering the board's cells
     int64_t y, w0;
     if (!ragged_chunk(nxw, H, y, w0)) return;
     const int lane = threadIdx.x & 63;
-    const int64_t wi = 2 + w0 + lane;
+    const int64_t wi = pad / 32 + w0 + lane;
     const uint32_t mine = w0 + lane < nxw && wi < pitch ? words[y * pitch + wi] : 0u;
     const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(cells + y * W, (short)0, (int)W, 0x00020000);
 #pragma unroll
@@ -467,28 +469,32 @@ hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W
     return hipGetLastError();
 }
 
-int64_t ring_pitch(int64_t W) { return 2 * ((W + 2 * kRingPad + 63) / 64); }
+int64_t ring_pitch(int64_t W, bool torus) { return 2 * ((W + (torus ? 2 * kRingPad : 0) + 63) / 64); }
 
-hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s) {
-    const int64_t pitch = ring_pitch(W);
+hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, bool torus,
+                            hipStream_t s) {
+    const int64_t pitch = ring_pitch(W, torus);
     if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gol_pack_ring, dim3(ragged_blocks(pitch, H)), dim3(256), 0, s, cells, words, W, H, pitch, ilv);
+    hipLaunchKernelGGL(gol_pack_ring, dim3(ragged_blocks(pitch, H)), dim3(256), 0, s, cells, words, W, H, pitch, ilv,
+                       torus ? kRingPad : (int64_t)0);
     return hipGetLastError();
 }
 
-hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, hipStream_t s) {
-    const int64_t pitch = ring_pitch(W);
+hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, bool torus,
+                              hipStream_t s) {
+    const int64_t pitch = ring_pitch(W, torus);
     if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad || (pitch + kChunkWords) * 32 >= ((int64_t)1 << 31))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(gol_unpack_ring, dim3(ragged_blocks(2 * ((W + 63) / 64), H)), dim3(256), 0, s, words, cells, W,
-                       H, pitch, ilv);
+                       H, pitch, ilv, torus ? kRingPad : (int64_t)0);
     return hipGetLastError();
 }
 
 hipError_t launch_ring_refresh(uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s) {
     if ((ilv != 1 && ilv != 2) || W < 3 * kRingPad) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gol_ring_refresh, dim3((unsigned)((H + 3) / 4)), dim3(256), 0, s, words, W, H, ring_pitch(W), ilv);
+    hipLaunchKernelGGL(gol_ring_refresh, dim3((unsigned)((H + 3) / 4)), dim3(256), 0, s, words, W, H, ring_pitch(W, true),
+                       ilv);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ struct StreamArgs {
     int32_t seam_opt;   // board option "seam": 0 = the engine's choice, < 0 = off
     int32_t rag_bits;   // ragged rows (width not a multiple of 32): cells in a row's last word (1..31); 0 otherwise
     int32_t rag_origin; // filled by plan_stream: ragged torus strips start at ring position -rag_origin
+    int64_t rag_w;      // bounded ragged rows: the board's width in cells (cells past it are dead); 0 otherwise
 };
 
 // ---- gol_step.hip
@@ -61,11 +62,14 @@ hipError_t launch_unpack_ragged(const uint32_t* words, uint8_t* cells, int64_t W
                                 hipStream_t s);
 hipError_t launch_unpack(const uint32_t* words, uint8_t* out, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                          int64_t stride, uint8_t value, int ilv, hipStream_t s);
-// Ring rows of a ragged torus board (gol_formats.hip): an aligned row of ring_pitch(W) words in layout ilv (1 or 2),
-// position u = cell (u - 64) mod W; pack / unpack against the byte board and the per-pass refresh of the two copies
-int64_t ring_pitch(int64_t W);
-hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s);
-hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, hipStream_t s);
+// Block rows of a ragged board (gol_formats.hip): aligned rows of ring_pitch(W, torus) words in layout ilv (1 or 2).
+// Torus: ring rows, position u = cell (u - 64) mod W; bounded: position u = cell u, zero past W.  Pack / unpack
+// against the byte board, and (torus) the per-pass refresh of the ring's two copies.
+int64_t ring_pitch(int64_t W, bool torus);
+hipError_t launch_pack_ring(const uint8_t* cells, uint32_t* words, int64_t W, int64_t H, int ilv, bool torus,
+                            hipStream_t s);
+hipError_t launch_unpack_ring(const uint32_t* words, uint8_t* cells, int64_t W, int64_t H, int ilv, bool torus,
+                              hipStream_t s);
 hipError_t launch_ring_refresh(uint32_t* words, int64_t W, int64_t H, int ilv, hipStream_t s);
 hipError_t launch_region(const void* board, int ilv, int64_t W, int64_t pitch, int64_t x0, int64_t y0, int64_t w,
                          int64_t h, uint8_t* out, hipStream_t s);

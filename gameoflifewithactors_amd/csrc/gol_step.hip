@@ -50,9 +50,9 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 // board narrower than one strip) also carries per-lane column masks, which spill at that budget (185 VGPRs;
 // round 1 measured 41k GCUPS with 12-wave workgroups, 74k with 8, profiles/r1/strip_bounded_sweep.log), so it
 // keeps 8.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int NARROW>
 struct Wpb {
-    static constexpr int value = !NARROW && K == 12 && M == 2 ? 12 : kWavesPerBlock;
+    static constexpr int value = NARROW != 1 && K == 12 && M == 2 ? 12 : kWavesPerBlock;
 };
 
 // Block-edge words of the neighbouring lanes, by DPP (a half-rate VALU move on gfx950,
@@ -169,10 +169,13 @@ struct TripRows {
 };
 
 // One wavefront's pipeline: K generation levels of 3-row windows of M-word blocks held in registers.
-// NARROW (bounded only): the board is narrower than one wave strip, so lanes can lie off the board and every
+// NARROW = 1 on a bounded board: the board is narrower than one wave strip, so lanes can lie off the board and every
 // level masks columns as well as rows.  Bounded boards at least a strip wide use edge-fill strips (no lane off
-// the board) and mask rows only: the column mask and its register are compiled out.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
+// the board) and mask rows only: the column mask and its register are compiled out -- unless NARROW = 2: a RAGGED
+// bounded row (width not a multiple of the block) on edge-fill strips, whose last block holds cells past the board's
+// edge (a.rag_w), so every level also ANDs the per-word column masks (all ones except on the lane holding that
+// block).  On a torus NARROW = 1 is the M = 1 ragged-row variant (kRagged).
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int NARROW>
 struct StreamWave {
     static constexpr int R = TripRows<K, M>::value;
     static_assert(R % 4 == 0, "slot roles must repeat every trip and registers alternate every two rows");
@@ -187,13 +190,14 @@ struct StreamWave {
     // (GameOfLifeDriver.fs:21-25): the lane holding word 0 takes its west carry from bit rag_bits - 1 of the word
     // before it, the lane holding the last word its east carry at bit rag_bits - 1 from the word after it, and the
     // last word's bits past the row are cleared every generation (DESIGN.md 4.1 "Ragged rows").
-    static constexpr bool kRagged = !BOUNDED && NARROW;
+    static constexpr bool kRagged = !BOUNDED && NARROW == 1;
+    static constexpr bool kRagEdge = BOUNDED && NARROW == 2;  // ragged bounded rows on edge-fill strips
     static_assert(!kRagged || (M == 1 && WRAP_ROWS), "ragged rows: single boards of consecutive words");
     static constexpr bool kNoHalo = K == 1 && !kRagged;
     static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
     // per-lane column masks: narrow (or ragged) bounded boards, and the K = 1 halo-free strips (their last strip
     // may end past the board's last block)
-    static constexpr bool kColMask = BOUNDED && (NARROW || kNoHalo);
+    static constexpr bool kColMask = BOUNDED && (NARROW != 0 || kNoHalo);
 
     // Seam strips (torus deep passes, a.seam): lanes 0..62 hold 63 consecutive blocks and all store; lane 63, the
     // SEAM lane, holds the first half of the block right of lane 62 (bits 0..15 of its words: cells 0..16M-1 of
@@ -224,7 +228,7 @@ struct StreamWave {
     const StreamArgs& a;
     int load_off;      // this lane's byte offset in a row (its block column; remainder waves: plus its sub-strip's rows)
     int store_off;     // = load_off for interior on-board lanes, kNoStore otherwise
-    uint32_t colmask;  // kColMask: ~0 for an on-board block
+    uint32_t colmask[M];  // kColMask: per word of the lane's block, its cells on the board (~0 inside, 0 off it)
     int64_t row_bytes;
     int64_t span_bytes;  // bytes a row descriptor covers: the row, or (remainder waves) every sub-strip's row
     // kStage: rows are prefetched straight to LDS (buffer_load_dword ... lds), not to registers: a second prefetch
@@ -306,6 +310,17 @@ struct StreamWave {
         return cut < 0 ? 0 : (cut > len ? len : cut);
     }
 
+    // Bounded boards: the cells of word j of block cb that lie on the board -- all of an inside block, none of an
+    // outside one, and of a ragged row's last block (a.rag_w cells per row, Script.fsx:6-13) the cells x < rag_w
+    // (word j bit b is cell 32 M cb + j + M b, gol_layout.h)
+    __device__ __forceinline__ uint32_t cell_mask(int64_t cb, int j, int64_t nblocks) const {
+        if (cb < 0 || cb >= nblocks) return 0u;
+        if (!a.rag_w) return 0xffffffffu;
+        const int64_t left = a.rag_w - 32 * M * cb - j;  // cells from this word's first cell to the row's end
+        const int64_t nbits = left <= 0 ? 0 : (left + M - 1) / M;
+        return nbits >= 32 ? 0xffffffffu : (1u << nbits) - 1u;
+    }
+
     // `lane`: lane within the wave's strip.  `role`: -1 = the wave owns segment sy; 0, 1, ... = the
     // oldest, next, ... wave of the SIMD group sharing group segment sy (split by a.split, see plan_stream)
     // `rem_count` > 0: a remainder wave of the seam geometry whose lanes hold rem_count sub-strips of (a.rem + 2)
@@ -322,16 +337,15 @@ struct StreamWave {
         // no column mask at any level.  Interior strips overlap by two blocks as on a torus (halo lanes).
         // this lane's block column (may be off-board)
         int64_t cb = kNoHalo ? sx * kWave + lane : sx * kInterior - 1 + lane;
-        if constexpr (BOUNDED && !kNoHalo && !NARROW) {  // the host picks NARROW exactly when nblocks < kWave
+        if constexpr (BOUNDED && !kNoHalo && NARROW != 1) {  // the host picks NARROW = 1 exactly when nblocks < kWave
             edge_fill = true;
             cb = (sx == a.nstrips - 1 ? nblocks - kWave : sx * kInterior) + lane;
         }
         int64_t lc;
         if (BOUNDED) {
             const bool in = cb >= 0 && cb < nblocks;
-            colmask = in ? 0xffffffffu : 0u;
-            // a ragged bounded row's last word: only its first rag_bits cells are on the board (Script.fsx:6-13)
-            if (a.rag_bits && cb == nblocks - 1) colmask = (1u << a.rag_bits) - 1u;
+#pragma unroll
+            for (int j = 0; j < M; j++) colmask[j] = cell_mask(cb, j, nblocks);
             lc = in ? cb : 0;
         } else if (kRagged) {
             // strips of 62 stored words over the ring positions -o .. nw - 1 - o (o = a.rag_origin: 1, or 2 when
@@ -340,13 +354,15 @@ struct StreamWave {
             // position 62 sx + l - 1 - o
             const int64_t p = sx * kInterior + lane - 1 - a.rag_origin;
             lc = floor_mod(p, nblocks);
-            colmask = 0xffffffffu;
+#pragma unroll
+            for (int j = 0; j < M; j++) colmask[j] = 0xffffffffu;
             cb = p;
             rag_shw = lc == 0 ? 32u - (uint32_t)a.rag_bits : 0u;
             rag_she = lc == nblocks - 1 ? (uint32_t)a.rag_bits - 1u : 31u;
             rag_mask = lc == nblocks - 1 ? (1u << a.rag_bits) - 1u : 0xffffffffu;
         } else {
-            colmask = 0xffffffffu;
+#pragma unroll
+            for (int j = 0; j < M; j++) colmask[j] = 0xffffffffu;
             lc = floor_mod(cb, nblocks);
         }
         load_off = (int)(lc * 4 * M);
@@ -358,7 +374,7 @@ struct StreamWave {
             int64_t nl;
             if (BOUNDED) {
                 const bool in = nbc >= 0 && nbc < nblocks;
-                nbmask = in ? 0xffffffffu : 0u;
+                nbmask = cell_mask(nbc, nbw, nblocks);
                 nl = in ? nbc : 0;
             } else {
                 nbmask = 0xffffffffu;
@@ -480,7 +496,7 @@ struct StreamWave {
             if (BOUNDED) {
                 const uint32_t rm = row_mask((int)first_step + r);
 #pragma unroll
-                for (int j = 0; j < M; j++) buf[r][j] = kColMask ? lut3<0x80>(buf[r][j], colmask, rm) : buf[r][j] & rm;
+                for (int j = 0; j < M; j++) buf[r][j] = kColMask ? lut3<0x80>(buf[r][j], colmask[j], rm) : buf[r][j] & rm;
                 if (kNoHalo) nb[r] = lut3<0x80>(nb[r], nbmask, rm);
             }
         }
@@ -626,7 +642,7 @@ struct StreamWave {
                 else if constexpr (kSeam)
                     v[r][j] = lut3<0xD8>(0xffff0000u, t.s[kSeam ? r : 0][j], v[r][j]);
                 else if constexpr (BOUNDED)
-                    v[r][j] = kColMask ? lut3<0x80>(v[r][j], colmask, rm) : v[r][j] & rm;
+                    v[r][j] = kColMask ? lut3<0x80>(v[r][j], colmask[j], rm) : v[r][j] & rm;
             }
         }
     }
@@ -651,7 +667,8 @@ struct StreamWave {
         for (int j = 0; j < M; j++) {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
             if (kRagged) out[j] &= rag_mask;
-            if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask, rowmask) : out[j] & rowmask;  // dead off the board
+            if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask[j], rowmask) : out[j] & rowmask;  // dead off the board
+            if (kRagEdge && !MASK) out[j] &= colmask[j];  // a ragged row's cells past its end, at every level
             sP[j] = sN[j];
             cP[j] = cN[j];
         }
@@ -757,7 +774,7 @@ struct StreamWave {
 };
 
 // Minimum waves per SIMD the register allocator must fit (1 = compiler's choice), per variant.
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int NARROW>
 struct MinWaves {
     static constexpr int value =
         Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value > 8 ? Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value / 4 : 1;
@@ -765,7 +782,7 @@ struct MinWaves {
 
 // Wave strips: Wpb waves per workgroup, each its own column strip and segment (or a share of a group
 // segment, see plan_stream).
-template <int K, int M, bool BOUNDED, bool WRAP_ROWS, bool NARROW>
+template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int NARROW>
 __global__ __launch_bounds__((kWave * Wpb<K, M, BOUNDED, WRAP_ROWS, NARROW>::value))
 __attribute__((amdgpu_waves_per_eu(MinWaves<K, M, BOUNDED, WRAP_ROWS, NARROW>::value)))
 void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, StreamArgs a) {
@@ -1022,31 +1039,35 @@ int stream_largest_k(int64_t n, int cap, int ilv) {
     return 1;
 }
 
-// The NARROW template flag: on a bounded board the column-masked variant, for boards narrower than one wave strip and
-// for ragged rows (rag_bits: cells in a ragged row's last word); on a torus the ragged-row variant (StreamWave
-// kRagged).
-static bool stream_narrow(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0) {
-    if (!bounded) return rag_bits != 0;
-    return k > 1 && (words / ilv < kWave || rag_bits != 0);
+// The NARROW template value of a pass.  Torus: 1 = the M = 1 ragged-row variant (StreamWave kRagged).  Bounded: 1 = a
+// board narrower than one wave strip (halo-lane strips, column masks at every level), 2 = a ragged row (rag_bits: the
+// board's width is not a multiple of 32; a.rag_w) at least a strip wide (edge-fill strips, column masks at every
+// level), 0 = edge-fill strips without column masks.
+static int stream_narrow(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0) {
+    if (!bounded) return rag_bits != 0 ? 1 : 0;
+    if (k <= 1) return 0;  // K = 1: halo-free strips with per-lane column masks anyway
+    if (words / ilv < kWave) return 1;
+    return rag_bits != 0 ? 2 : 0;
 }
 
 // Variants: torus with rows wrapping in the buffer (single board), torus strip with ghost rows, ragged torus rows
 // (single board, ilv 1), bounded (never wraps: rows beyond the board are masked dead; narrow and ragged boards
 // mask columns too).
 template <int K, int M>
-static const void* stream_kernel(bool bounded, bool wrap, bool narrow) {
+static const void* stream_kernel(bool bounded, bool wrap, int narrow) {
     if (bounded)
-        return narrow ? (const void*)&gol_stream_step<K, M, true, false, true>
-                      : (const void*)&gol_stream_step<K, M, true, false, false>;
+        return narrow == 1 ? (const void*)&gol_stream_step<K, M, true, false, 1>
+                           : (narrow == 2 ? (const void*)&gol_stream_step<K, M, true, false, 2>
+                                          : (const void*)&gol_stream_step<K, M, true, false, 0>);
     if (narrow) {
-        if constexpr (M == 1) return wrap ? (const void*)&gol_stream_step<K, 1, false, true, true> : nullptr;
+        if constexpr (M == 1) return wrap ? (const void*)&gol_stream_step<K, 1, false, true, 1> : nullptr;
         return nullptr;
     }
-    return wrap ? (const void*)&gol_stream_step<K, M, false, true, false>
-                : (const void*)&gol_stream_step<K, M, false, false, false>;
+    return wrap ? (const void*)&gol_stream_step<K, M, false, true, 0>
+                : (const void*)&gol_stream_step<K, M, false, false, 0>;
 }
 
-static const void* kernel_for(int k, int ilv, bool bounded, bool wrap, bool narrow) {
+static const void* kernel_for(int k, int ilv, bool bounded, bool wrap, int narrow) {
 #define GOL_KPTR(K_, M_) \
     if (k == K_ && ilv == M_) return stream_kernel<K_, M_>(bounded, wrap, narrow);
     GOL_FOR_EACH_KM(GOL_KPTR)
@@ -1060,19 +1081,20 @@ int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits)
     if (k == 1) return (nblocks + kWave - 1) / kWave;  // K = 1: halo-free strips
     // bounded edge-fill strips (StreamWave::edge_fill): strip 0 stores blocks [0, 63), strip s stores
     // [62 s + 1, 62 s + 63), the last ends at the board's last block
-    if (bounded && nblocks >= kWave && !rag_bits) return (nblocks - 1 + kInterior - 1) / kInterior;
-    // halo-lane strips (torus; bounded NARROW: narrow or ragged rows): strip s stores blocks [62 s, 62 s + 62)
+    if (bounded && nblocks >= kWave) return (nblocks - 1 + kInterior - 1) / kInterior;
+    // halo-lane strips (torus; bounded NARROW = 1: narrow rows): strip s stores blocks [62 s, 62 s + 62)
     return (nblocks + kInterior - 1) / kInterior;
 }
 
 // Waves per workgroup of a variant (Wpb)
 int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits) {
-    const bool narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
+    const int narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
 #define GOL_WPBQ(K_, M_)                                                                                 \
     if (k == K_ && ilv == M_)                                                                            \
-        return bounded ? (narrow ? Wpb<K_, M_, true, false, true>::value : Wpb<K_, M_, true, false, false>::value) \
-                       : (narrow ? Wpb<K_, M_, false, true, true>::value                                  \
-                                 : (wrap ? Wpb<K_, M_, false, true, false>::value : Wpb<K_, M_, false, false, false>::value));
+        return bounded ? (narrow == 1 ? Wpb<K_, M_, true, false, 1>::value                               \
+                                      : (narrow == 2 ? Wpb<K_, M_, true, false, 2>::value : Wpb<K_, M_, true, false, 0>::value)) \
+                       : (narrow ? Wpb<K_, M_, false, true, 1>::value                                     \
+                                 : (wrap ? Wpb<K_, M_, false, true, 0>::value : Wpb<K_, M_, false, false, 0>::value));
     GOL_FOR_EACH_KM(GOL_WPBQ)
 #undef GOL_WPBQ
     return kWavesPerBlock;
@@ -1104,11 +1126,11 @@ int stream_pair_split(int k, int ilv, bool bounded) {
 // Waves of a stream-kernel variant the current device holds at once (occupancy x CUs), cached.  Falls back
 // to 4096 waves when no device answers (host-only planning, e.g. CPU tests).
 static int64_t resident_units(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits) {
-    static std::atomic<int64_t> cache[33][5][2][2][2];
+    static std::atomic<int64_t> cache[33][5][2][2][3];
     const int64_t fallback = 4096;
     if (k < 0 || k > 32 || ilv < 1 || ilv > 4) return fallback;
     if (bounded) wrap = false;
-    const bool narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
+    const int narrow = stream_narrow(words, ilv, k, bounded, rag_bits);
     int64_t v = cache[k][ilv][bounded][wrap][narrow].load(std::memory_order_relaxed);
     if (v > 0) return v;
     const void* fn = kernel_for(k, ilv, bounded, wrap, narrow);
@@ -1224,22 +1246,25 @@ static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs
     const unsigned blocks = (unsigned)((waves + WPB - 1) / WPB);
     const dim3 block(kWave * WPB);
     if (bounded) {
-        if (stream_narrow(a.words, M, K, true, a.rag_bits))
-            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, true>), dim3(blocks), block, 0, s, src, dst, a);
+        const int narrow = stream_narrow(a.words, M, K, true, a.rag_bits);
+        if (narrow == 1)
+            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, 1>), dim3(blocks), block, 0, s, src, dst, a);
+        else if (narrow == 2)
+            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, 2>), dim3(blocks), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, true, false, 0>), dim3(blocks), block, 0, s, src, dst, a);
     } else if (a.rag_bits) {
         if constexpr (M == 1) {
             if (!wrap) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((gol_stream_step<K, 1, false, true, true>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, 1, false, true, 1>), dim3(blocks), block, 0, s, src, dst, a);
         } else {
             return hipErrorInvalidValue;
         }
     } else {
         if (wrap)
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, true, false>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, true, 0>), dim3(blocks), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_stream_step<K, M, false, false, false>), dim3(blocks), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_stream_step<K, M, false, false, 0>), dim3(blocks), block, 0, s, src, dst, a);
     }
     return hipGetLastError();
 }

@@ -44,7 +44,7 @@ def _run(gol, b0, boundary, steps, stream, tblock_k=0, ring=1):
 WIDTHS = [8193, 8209, 8223, 10001, 62 * 133 * 32 - 31, 62 * 134 * 32 + 5, 16383]
 
 
-@pytest.mark.parametrize("boundary,ring", [(0, 1), (0, 0), (1, 1)])
+@pytest.mark.parametrize("boundary,ring", [(0, 1), (0, 0), (1, 1), (1, 0)])
 @pytest.mark.parametrize("w", WIDTHS)
 def test_ragged_stream_matches_oracle(gol, oracle, w, boundary, ring):
     h = 70
@@ -56,11 +56,14 @@ def test_ragged_stream_matches_oracle(gol, oracle, w, boundary, ring):
 
 # ring rows at ilv 2 (above 2^25 ring cells): the widths' last 64-cell block holds 1 .. 63 of the board's cells, the
 # seam geometry (>= 63 blocks) and not
+@pytest.mark.parametrize("boundary", [0, 1])
 @pytest.mark.parametrize("w", [8193, 8255, 10001, 16383, 16447, 4033 * 8 + 1])
-def test_ragged_ring_interleaved(gol, oracle, w):
+def test_ragged_ring_interleaved(gol, oracle, w, boundary):
+    """Block rows at ilv 2 against the ilv-1 rows and the oracle's light cone.  Bounded: edge-fill strips whose last
+    block is partial (1 .. 63 of its cells on the board), masked at every level (gol_step.hip NARROW = 2)."""
     h = (1 << 25) // w + 40
     b0 = _rand(h, w, w, p=0.3)
-    with gol.Board(w, h, 0, options={"coop": 0}) as b:
+    with gol.Board(w, h, boundary, options={"coop": 0}) as b:
         assert b.info()["tblock_k"] == 16
         b.set_cells(b0).step(16 + 12 + 5)
         got_rows = b.get_region(0, 0, w, 64)
@@ -69,11 +72,16 @@ def test_ragged_ring_interleaved(gol, oracle, w):
         b.set_cells(b0).step(16 + 12 + 5)
         np.testing.assert_array_equal(b.get_region(0, 0, w, 64), got_rows)
         np.testing.assert_array_equal(b.get_region(0, h - 40, w, 40), got_end)
-    # the first 64 rows against the oracle's light cone (the torus rows wrap: rows h-33 .. h-1 above row 0)
     gens = 33
-    win = np.concatenate([b0[h - gens:], b0[:64 + gens]], axis=0)
-    sub = oracle.c_run(np.ascontiguousarray(win), gens, 0)  # the window's own y wrap only pollutes the cone edges
-    np.testing.assert_array_equal(got_rows, sub[gens:gens + 64])
+    if boundary == 0:
+        # the first 64 rows against the oracle's light cone (the torus rows wrap: rows h-33 .. h-1 above row 0)
+        win = np.concatenate([b0[h - gens:], b0[:64 + gens]], axis=0)
+        sub = oracle.c_run(np.ascontiguousarray(win), gens, 0)  # the window's own y wrap only pollutes the cone edges
+        np.testing.assert_array_equal(got_rows, sub[gens:gens + 64])
+    else:
+        # bounded: rows 0..63 depend only on rows 0..63+gens (dead above the board); bounded x edges are exact
+        sub = oracle.c_run(np.ascontiguousarray(b0[:64 + gens]), gens, 1)
+        np.testing.assert_array_equal(got_rows, sub[:64])
 
 
 @pytest.mark.parametrize("k", [1, 2, 8, 16, 24, 32])

@@ -1,6 +1,7 @@
 """Ragged boards past the cooperative pass (width not a multiple of 32, wider than 8192 or above 2^26 cells), passes
-interleaved on one box: ring rows on the aligned kernel (torus, board option ragged_ring=1, the default), the M = 1
-ragged-row variant (ragged_ring=0), and optionally the per-generation byte step (ragged_stream=0).  Timing: the
+interleaved on one box: block rows in the aligned layouts (board option ragged_ring=1, the default: ring rows on a
+torus, column-masked rows when bounded), the ilv-1 rows (ragged_ring=0), and optionally the per-generation byte step
+(ragged_stream=0).  Timing: the
 library's own HIP events around one gol_step call (gol_step_timed; no torch in the process), after 40 warm-up
 generations; the state stays in the scratch rows between the calls (DESIGN.md 4.1 "Ragged rows").  One JSON line per
 (board, boundary, pass, depth, round).
@@ -37,8 +38,6 @@ def main():
             for boundary in (int(x) for x in a.boundaries.split(",")):
                 for k in (int(x) for x in a.ks.split(",")):
                     for name in a.passes.split(","):
-                        if name == "m1" and boundary == 1:
-                            continue  # bounded boards have one streaming variant
                         g = gens if name != "bytestep" else max(4, gens // 10)
                         with Board(w, h, boundary, tblock_k=k, options=OPTS[name]) as b:
                             b.seed_splitmix(0x5EED)
