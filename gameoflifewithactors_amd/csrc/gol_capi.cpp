@@ -260,6 +260,7 @@ struct gol_board {
     int rag_cur = 0;
     int64_t rag_pitch = 0;
     int rag_ilv = 1;
+    int ring_age = 0;  // ring rows: generations since the copies were last exact (errors reach ring_age cells in)
     int64_t generation = 0;
     gol::MultiBoard* multi = nullptr;  // num_gpus > 1: row strips over several devices (gol_multi.h)
 
@@ -561,6 +562,7 @@ bool use_stream_ragged(const gol_board* b) {
 // that AND per-word column masks at every level (gol_step.hip NARROW = 2).  Layout and depth follow the aligned rules
 // for a board of that many cells (board_ilv / board_tblock): ilv 2 from 2^25 cells, K = 16 below 2^29, 12 above.
 bool use_ring(const gol_board* b) { return b->opt.ragged_ring; }
+constexpr int kRingCopy = 64;  // cells copied at each end of a ring row (gol_formats.hip kRingPad; the suffix has >= 64)
 int64_t ring_cells(int64_t W, int64_t H, int boundary) { return gol::ring_pitch(W, boundary == GOL_TORUS) * 32 * H; }
 int ring_ilv(const gol_board* b) { return ring_cells(b->W, b->H, b->boundary) < kSmallBoardCells ? 1 : 2; }
 
@@ -615,6 +617,7 @@ int step_impl(gol_board* b, int64_t gens) {
             if (int rc = ensure_rag(b, pitch * b->H)) return rc;
             GOL_HIP(gol::launch_pack_ring(b->cells(b->cur), b->rag[0], b->W, b->H, ilv, torus, b->stream));
             b->rag_cur = 0;
+            b->ring_age = 0;
         }
         b->rag_state = 3;
         b->rag_pitch = pitch;
@@ -629,8 +632,14 @@ int step_impl(gol_board* b, int64_t gens) {
                 a.rag_bits = (int32_t)(b->W % 32);
                 a.rag_w = b->W;
             }
+            // ring rows: the errors from the extended row's ends spread k cells per pass; refresh the copies before
+            // a pass would carry them past the 64 copied cells into the board's own
+            if (torus && b->ring_age + k > kRingCopy) {
+                GOL_HIP(gol::launch_ring_refresh(b->rag[b->rag_cur], b->W, b->H, ilv, b->stream));
+                b->ring_age = 0;
+            }
             GOL_HIP(gol::launch_stream_step(b->rag[b->rag_cur], b->rag[b->rag_cur ^ 1], a, k, !torus, torus, b->stream));
-            if (torus) GOL_HIP(gol::launch_ring_refresh(b->rag[b->rag_cur ^ 1], b->W, b->H, ilv, b->stream));
+            b->ring_age += k;
             b->rag_cur ^= 1;
             b->generation += k;
             gens -= k;

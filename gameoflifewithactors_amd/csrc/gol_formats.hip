@@ -193,9 +193,12 @@ __global__ __launch_bounds__(256) void gol_unpack_ring(const uint32_t* __restric
     }
 }
 
-// After a pass: rewrite the copies at both ends of every ring row from the board's cells (u-block 0 <- positions
-// u + W; positions u >= 64 + W <- u - W; the board's own cells in the first suffix block are kept).  One wavefront per
-// row; every source position lies in [64, 64 + W), which this kernel never writes.
+// Rewrite the copies at both ends of every ring row from the board's cells (u-block 0 <- positions u + W; positions
+// u >= 64 + W <- u - W; the board's own cells in the first suffix block are kept): at most 4 blocks per row (the
+// suffix spans 64 .. 127 positions).  One wavefront per row; every lane issues its (at most 4) loads before the first
+// ballot, so a row costs one memory round trip.  Every source position lies in [64, 64 + W), which this kernel never
+// writes.  The host runs it only when the errors from the extended row's two ends could reach the board's cells on
+// the next pass: they spread one cell per generation, so every 64 / k passes (gol_capi.cpp ring_age).
 __global__ __launch_bounds__(256) void gol_ring_refresh(uint32_t* __restrict__ words, int64_t W, int64_t H,
                                                         int64_t pitch, int ilv) {
     const int64_t y = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -204,12 +207,20 @@ __global__ __launch_bounds__(256) void gol_ring_refresh(uint32_t* __restrict__ w
     uint32_t* row = words + y * pitch;
     const int64_t nblk = pitch / 2, end = kRingPad + W;
     const int64_t first_suffix = end >> 6;
-    for (int64_t c = -1; c < nblk; c = c < 0 ? first_suffix : c + 1) {
-        const int64_t cb = c < 0 ? 0 : c;
+    uint32_t bit[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int64_t cb = i == 0 ? 0 : first_suffix + i - 1;
+        if (cb >= nblk) continue;  // wave-uniform
         const int64_t u = cb * 64 + lane;
-        const int64_t src = c < 0 ? u + W : (u >= end ? u - W : u);
-        const uint64_t m = __ballot(ring_bit(row, src, ilv) != 0);
-        __builtin_amdgcn_wave_barrier();
+        const int64_t src = i == 0 ? u + W : (u >= end ? u - W : u);
+        bit[i] = ring_bit(row, src, ilv);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int64_t cb = i == 0 ? 0 : first_suffix + i - 1;
+        if (cb >= nblk) continue;
+        const uint64_t m = __ballot(bit[i] != 0);
         if (lane < 2) row[2 * cb + lane] = ring_word(m, lane, ilv);
     }
 }
