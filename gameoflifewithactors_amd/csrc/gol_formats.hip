@@ -137,11 +137,25 @@ __device__ __forceinline__ uint32_t even_bits64(uint64_t x) {
 __device__ __forceinline__ uint32_t ring_word(uint64_t m, int p, int ilv) {
     return ilv == 2 ? even_bits64(m >> p) : (uint32_t)(m >> (32 * p));
 }
+#ifndef GOL_CHECK_BOUNDS
+#define GOL_CHECK_BOUNDS 0  // diagnostic builds: flag an access outside its row (gol_step.hip gol_debug_bounds)
+#endif
+#if GOL_CHECK_BOUNDS
+__device__ unsigned g_bounds_err_formats;
+#endif
 // bit of ring position u of a row
-__device__ __forceinline__ uint32_t ring_bit(const uint32_t* row, int64_t u, int ilv) {
+__device__ __forceinline__ uint32_t ring_bit(const uint32_t* row, int64_t u, int ilv, int64_t pitch = 0) {
     const int64_t c = u >> 6;
     const int i = (int)(u & 63);
     const int64_t w = 2 * c + (ilv == 2 ? (i & 1) : (i >> 5));
+#if GOL_CHECK_BOUNDS
+    if (w < 0 || w >= pitch) {
+        __hip_atomic_fetch_or(&g_bounds_err_formats, 1u << 20, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+#else
+    (void)pitch;
+#endif
     return (row[w] >> (ilv == 2 ? (i >> 1) : (i & 31))) & 1u;
 }
 
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(256) void gol_ring_refresh(uint32_t* __restrict__ w
         if (cb >= nblk) continue;  // wave-uniform
         const int64_t u = cb * 64 + lane;
         const int64_t src = i == 0 ? u + W : (u >= end ? u - W : u);
-        bit[i] = ring_bit(row, src, ilv);
+        bit[i] = ring_bit(row, src, ilv, pitch);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -585,3 +599,12 @@ hipError_t launch_set_points(void* board, int ilv, int64_t W, int64_t pitch, con
 }
 
 }  // namespace gol
+
+#if GOL_CHECK_BOUNDS
+extern "C" unsigned gol_debug_bounds_formats(void) {
+    unsigned v = 0, z = 0;
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(gol::g_bounds_err_formats), sizeof(v), 0, hipMemcpyDeviceToHost);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gol::g_bounds_err_formats), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    return v;
+}
+#endif

@@ -31,6 +31,9 @@
 #include "gol_layout.h"
 #include "gol_internal.h"
 
+#if GOL_CHECK_BOUNDS
+extern "C" unsigned gol_debug_bounds_formats(void);  // gol_formats.hip
+#endif
 namespace gol {
 
 static constexpr int kWave = 64;
@@ -160,6 +163,31 @@ struct Vec<4> {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint32_t* row, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(row), (short)0, (int)bytes, kRsrcWord3);
 }
+// GOL_CHECK_BOUNDS (diagnostic builds only, never shipped): every descriptor's [base, base + range) is checked
+// against the buffer it addresses; a violation sets bit `tag` of g_bounds_err (gol_debug_bounds reads and clears it)
+// and the descriptor gets range 0, so the access is dropped instead of faulting.
+#ifndef GOL_CHECK_BOUNDS
+#define GOL_CHECK_BOUNDS 0
+#endif
+#if GOL_CHECK_BOUNDS
+__device__ unsigned g_bounds_err;
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t checked_rsrc(const void* base, int64_t bytes, const void* buf,
+                                                               int64_t buf_bytes, int tag) {
+#if GOL_CHECK_BOUNDS
+    const int64_t off = (const char*)base - (const char*)buf;
+    if (bytes > 0 && (off < 0 || off + bytes > buf_bytes)) {
+        if ((threadIdx.x & 63) == 0)  // a vector atomic (lane-dependent branch)
+            __hip_atomic_fetch_or(&g_bounds_err, 1u << tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bytes = 0;
+    }
+#else
+    (void)buf;
+    (void)buf_bytes;
+    (void)tag;
+#endif
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
+}
 
 // Rows per loop trip (even, and a multiple of 4 so register roles repeat every trip): enough loads in
 // flight for the memory-bound K = 1 pass, fewer for the deep passes whose registers hold the windows.
@@ -264,6 +292,13 @@ struct StreamWave {
         return kDmas == 1 ? (*stage)[par][kind][r][0][lane * kDmaWords + j] : (*stage)[par][kind][r][j][lane];
     }
     int64_t seg_begin, seg_end, nsteps, ly0;
+    __device__ __forceinline__ int64_t buf_bytes() const { return (a.rows + 2 * a.ghost) * a.pitch * 4; }
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t src_rs(const uint32_t* base, int64_t bytes, int tag) const {
+        return checked_rsrc(base, bytes, src, buf_bytes(), tag);
+    }
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t dst_rs(const void* base, int64_t bytes, int tag) const {
+        return checked_rsrc(base, bytes, dst, buf_bytes(), tag);
+    }
     // kStage walks, wave-uniform (SGPRs): a bounded board's next row to load (byte address and step index; rows
     // outside [step_lo, step_hi] load nothing), and every variant's next output row to store (byte address and step
     // relative to seg_begin)
@@ -491,8 +526,8 @@ struct StreamWave {
                 load_br = br + 1;
                 br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
             }
-            V::load(row_rsrc(src + br * a.pitch, span_bytes), load_off, buf[r]);
-            if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(row_rsrc(src + br * a.pitch, row_bytes), nb_off, 0, 0);
+            V::load(src_rs(src + br * a.pitch, span_bytes, 1), load_off, buf[r]);
+            if (kNoHalo) nb[r] = __builtin_amdgcn_raw_buffer_load_b32(src_rs(src + br * a.pitch, row_bytes, 2), nb_off, 0, 0);
             if (BOUNDED) {
                 const uint32_t rm = row_mask((int)first_step + r);
 #pragma unroll
@@ -535,17 +570,17 @@ struct StreamWave {
         const uint32_t* base = src + br0 * a.pitch;
         if (WRAP_ROWS) {
             if (br0 + R <= a.rows) {
-                dma<1>(row_rsrc(base, R * pb), lds, seam1_delta);
+                dma<1>(src_rs(base, R * pb, 3), lds, seam1_delta);
             } else {
                 const int n1 = (int)((a.rows - br0) * pb);  // bytes of the rows before the wrap (>= one row)
                 if (seam1_delta < n1)
-                    dma<1>(row_rsrc(base, n1), lds, seam1_delta);
+                    dma<1>(src_rs(base, n1, 4), lds, seam1_delta);
                 else
-                    dma<1>(row_rsrc(src, R * pb), lds, seam1_delta - n1);
+                    dma<1>(src_rs(src, R * pb, 5), lds, seam1_delta - n1);
             }
         } else {
             const int64_t left = (a.rows + 2 * a.ghost - br0) * pb;
-            dma<1>(row_rsrc(base, left < R * pb ? left : R * pb), lds, seam1_delta);
+            dma<1>(src_rs(base, left < R * pb ? left : R * pb, 6), lds, seam1_delta);
         }
     }
     template <int PAR, int KINDS>
@@ -558,8 +593,7 @@ struct StreamWave {
             __amdgpu_buffer_rsrc_t rs;
             if constexpr (BOUNDED) {
                 const bool inside = lrow >= step_lo && lrow <= step_hi;
-                rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(lptr), (short)0, inside ? (int)span_bytes : 0,
-                                                       kRsrcWord3);
+                rs = src_rs(reinterpret_cast<const uint32_t*>(lptr), inside ? span_bytes : 0, 7);
                 lptr += (uint64_t)a.pitch * 4;
                 lrow++;
             } else {
@@ -571,7 +605,7 @@ struct StreamWave {
                     load_br = br + 1;
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
-                rs = row_rsrc(src + br * a.pitch, span_bytes);
+                rs = src_rs(src + br * a.pitch, span_bytes, 8);
                 if constexpr (kSeam1)
                     if (r == 0) stage_load_seam1<PAR>(br);
             }
@@ -598,8 +632,7 @@ struct StreamWave {
         for (int r = 0; r < R; r++) {
             const int d = sd + r;
             const bool valid = d >= 0 && d < seglen;
-            V::store(__builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sptr + r * pitch_bytes), (short)0,
-                                                       valid ? (int)span_bytes : 0, kRsrcWord3),
+            V::store(dst_rs(reinterpret_cast<void*>(sptr + r * pitch_bytes), valid ? span_bytes : 0, 9),
                      store_off, v[r]);
         }
         sptr += R * pitch_bytes;
@@ -749,7 +782,7 @@ struct StreamWave {
     }
 
     __device__ __forceinline__ void store_row(const uint32_t (&v)[M], int64_t row, bool valid) {
-        V::store(row_rsrc(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? span_bytes : 0), store_off, v);
+        V::store(dst_rs(dst + ((WRAP_ROWS ? 0 : a.ghost) + row) * a.pitch, valid ? span_bytes : 0, 10), store_off, v);
     }
     // Store trip t's outputs.  Rows outside the segment (pipeline fill and the tail) get an empty
     // descriptor (num_records 0): the stores are dropped by the range check with no branch, and the row
@@ -1282,6 +1315,15 @@ hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, 
 
 }  // namespace gol
 
+#if GOL_CHECK_BOUNDS
+extern "C" unsigned gol_debug_bounds(void) {  // diagnostic builds: violation bits of the step kernels, then cleared
+    unsigned v = 0, z = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(gol::g_bounds_err), sizeof(v), 0, hipMemcpyDeviceToHost);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gol::g_bounds_err), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    return v | gol_debug_bounds_formats();
+}
+#endif
 #if GOL_STAMP
 extern "C" int gol_debug_stamps(unsigned long long* out, long long n) {
     if (n > 2 * gol::kStamps) n = 2 * gol::kStamps;

@@ -34,3 +34,22 @@ def oracle():
     import gol_oracle
 
     return gol_oracle
+
+
+@pytest.fixture(autouse=True)
+def _bounds_check_build(request):
+    """Diagnostic builds only (GOL_LIB=<a library built with -DGOL_CHECK_BOUNDS=1>): after every test, fail it if any
+    kernel built a buffer descriptor reaching outside its buffer (gol_debug_bounds).  The shipped library has no such
+    symbol and this does nothing."""
+    yield
+    if "gpu" not in request.keywords or "GOL_LIB" not in os.environ:
+        return
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    fn = getattr(lib, "gol_debug_bounds", None)
+    if fn is None:
+        return
+    fn.restype = __import__("ctypes").c_uint
+    bits = fn()
+    assert bits == 0, f"out-of-buffer descriptor in this test: tag bits {bits:#x} (gol_step.hip checked_rsrc tags)"
