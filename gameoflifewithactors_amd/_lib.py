@@ -116,6 +116,7 @@ SIGNATURES = {
     "gol_strip_hash_partial": (ctypes.c_int, [sp, vp, vp, vp]),
     "gol_hash_finalize": (u64, [u64, i64, i64]),
     "gol_strip_plan": (ctypes.c_int, [sp, ctypes.c_int, i64, i64, i64p, i64p]),
+    "gol_strip_plan_ex": (ctypes.c_int, [sp, ctypes.c_int, i64, i64, i64p, i64]),
     "gol_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64]),
     "gol_transport": (ctypes.c_int, [vp, ip, ctypes.c_char_p, i64]),
     "gol_exchange_plan": (ctypes.c_int, [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, ctypes.POINTER(Xfer), i64,

@@ -1462,6 +1462,18 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
     return gol::strip_plan_opts(s, k, out_begin, out_end, waves, seg_rows, 0, 0, 0);
 }
 
+int gol_strip_plan_ex(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* plan, int64_t n) {
+    if (int rc = check_strip(s)) return rc;
+    if (!plan || n < 8) return fail(GOL_ERR_INVALID, "plan needs 8 entries");
+    if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, 0, 0, 0);
+    gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
+    const int64_t v[8] = {a.nstrips, a.nsegs, a.seg, a.seam, a.rem, a.rem_p, a.rem_mid, a.rem_units};
+    for (int i = 0; i < 8; i++) plan[i] = v[i];
+    return GOL_OK;
+}
+
 int gol_strip_step(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin,
                    int64_t out_end, void* stream) {
     return gol::strip_step_opts(s, src, dst, k, out_begin, out_end, (hipStream_t)stream, 0, 0, 0);

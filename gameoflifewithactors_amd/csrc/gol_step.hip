@@ -1259,9 +1259,20 @@ void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
         const int64_t fit = 1 + ((((int64_t)1 << 31) - 1 - row_bytes) / step);
         if (a.rem_p > fit) a.rem_p = (int32_t)(fit > 1 ? fit : 1);
         // segments 1 .. rem_mid share remainder waves: every row they stream must lie in the board / buffer
-        // without a wrap (a single board's last segment shorter than k would push its neighbour's halo past it)
+        // without a wrap.  Sub-strip j reads its rows at a fixed offset from sub-strip 0's walk, which wraps (single
+        // board) or clamps (ghost-row strip) only for itself; so the last packed segment's rows -- its k halo rows
+        // below and the walk's overshoot -- must end inside the buffer.  The walk prefetches whole trips of R = 4
+        // rows, one trip ahead, and the last trip prefetches one more (unused): ceil((seg + 2k) / 4) + 1 trips, up to
+        // 7 rows past the seg + 2k the segment streams.  Round 3 let those rows run past the buffer's end: reads
+        // beyond the allocation, harmless unless the next page was unmapped -- an illegal-address fault in round 4's
+        // suite on an 8209 x 40 ragged board (ring rows of 262 words, 42 KB), found by the GOL_CHECK_BOUNDS build
+        // (descriptor tag 8) and reproduced on the CPU by walking the plan.
+        const int64_t trip = 4;  // TripRows of every seam pass (K > 1)
+        const int64_t over = ((seg + 2 * k + trip - 1) / trip + 1) * trip - (seg + 2 * k);
+        const int64_t limit = wrap ? a.rows : a.rows + a.ghost;  // first row index past the buffer (owned-row units)
         int64_t mid = a.nsegs - 2;
-        if (wrap && a.nsegs >= 3 && rows - (a.nsegs - 1) * seg < k) mid = a.nsegs - 3;
+        const int64_t fit_mid = (limit - a.out_begin - k - over) / seg - 1;  // (m + 1) seg + k + over <= limit - out_begin
+        if (fit_mid < mid) mid = fit_mid;
         // sub-strip j streams rows [(j + 1) seg - k, (j + 2) seg + k) of the buffer at a fixed offset from
         // sub-strip 0's walk: a segment shorter than k (the "seg_rows" option can ask for one) would make segment 1's
         // first rows wrap or leave the buffer, so such segments run as lone remainder units

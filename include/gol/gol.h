@@ -243,6 +243,11 @@ int gol_exchange_plan(int64_t height, int boundary, int nparts, int64_t ghost, i
 /* Number of wavefront column strips / rows per segment the step kernel uses (for roofline accounting). */
 int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves,
                    int64_t* seg_rows);
+/* The whole plan (n >= 8): plan[0..7] = column strips, row segments, rows per segment, seam geometry (1 / 0),
+ * remainder blocks per row, remainder sub-strips per wave, packed remainder segments (segments 1 .. plan[6] share
+ * remainder waves), remainder units.  Planned for the current device's resident waves (4096 without a device):
+ * tests/test_cpu_host.py walks it to check that no wave reads outside its buffer. */
+int gol_strip_plan_ex(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* plan, int64_t n);
 
 #ifdef __cplusplus
 }

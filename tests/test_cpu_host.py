@@ -182,3 +182,58 @@ def test_native_host_mirror_fails_loudly_without_gpu():
     out = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stdout + out.stderr
     assert '"failures": []' in out.stdout
+
+
+def _walk_rows(plan, k, rows, ghost, wrap, out_begin, out_end, trip=4):
+    """Every buffer row each wave of the seam geometry reads (csrc/gol_step.hip StreamWave + the unit mapping in
+    gol_stream_step): sub-strip 0's walk wraps (single board) or clamps (ghost-row strip) for itself, sub-strip j reads
+    j * seg rows further; the walk prefetches ceil((len + 2k) / 4) + 1 trips of 4 rows."""
+    nstrips, nsegs, seg, seam, rem, rem_p, rem_mid, rem_units = plan
+    buf_rows = rows if wrap else rows + 2 * ghost
+    packed = (rem_mid + rem_p - 1) // rem_p
+    for r in range(rem_units):
+        if 1 <= r <= packed:
+            sy = 1 + (r - 1) * rem_p
+            count = min(1 + rem_mid - sy, rem_p)
+        else:
+            sy = 0 if r == 0 else r - packed + rem_mid
+            count = 1
+        b = out_begin + sy * seg
+        e = min(b + seg, out_end)
+        nsteps = (e - b) + 2 * k
+        br = (b - k) % rows if wrap else b - k + ghost
+        for _ in range(((nsteps + trip - 1) // trip + 1) * trip):
+            row = br if wrap else min(max(br, 0), buf_rows - 1)
+            for j in range(count):
+                yield r, sy, j, row + j * seg, buf_rows
+            br = (0 if br + 1 == rows else br + 1) if wrap else br + 1
+
+
+@pytest.mark.parametrize("words,ilv,k", [(64, 1, 8), (64, 1, 4), (262, 1, 8), (262, 2, 12), (2052, 2, 12),
+                                         (1026, 2, 16), (128, 2, 8), (200, 1, 2)])
+def test_seam_remainder_waves_stay_inside_the_buffer(words, ilv, k):
+    """Round 4: packed remainder sub-strips of the seam geometry read past the buffer's end (the walk's last,
+    unused prefetch trip) -- an illegal-address fault when the next page was unmapped (an 8209 x 40 ragged board).
+    The library's own plan (gol_strip_plan_ex, planned here for 4096 resident waves) must keep every row a wave
+    reads inside its buffer, on single boards (rows wrap) and ghost-row strips (interior and edge launches)."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    for rows in list(range(20, 200, 3)) + [300, 1500, 2048, 4099]:
+        for wrap in (True, False):
+            ghost = 0 if wrap else k
+            strip = _lib.Strip(words * 32, rows if wrap else rows * 3, 0 if wrap else rows, rows, ghost,
+                               words, 0, 1 if wrap else 0, ilv, 0)
+            launches = [(0, rows)] if wrap else [(0, rows), (k, rows - k), (0, k), (rows - k, rows)]
+            for b, e in launches:
+                if e <= b:
+                    continue
+                plan = (ctypes.c_int64 * 8)()
+                assert lib.gol_strip_plan_ex(ctypes.byref(strip), k, b, e, plan, 8) == 0, lib.gol_last_error()
+                plan = list(plan)
+                if not plan[3] or not plan[4]:
+                    continue
+                for r, sy, j, row, buf_rows in _walk_rows(plan, k, rows, ghost, wrap, b, e):
+                    assert 0 <= row < buf_rows, (rows, wrap, (b, e), plan, r, sy, j, row)
