@@ -105,6 +105,7 @@ def parse():
                    "with every strip on device 0), timed by rank 0 after the main leg and hashed at the main leg's "
                    "verify generation; -1 = the world size (1: the single board); 0 = off")
     p.add_argument("--verify-gen", type=int, default=-1, help=argparse.SUPPRESS)
+    p.add_argument("--handle-first-gen", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-verify", action="store_true",
                    help="skip the untimed self-check (step to the next golden checkpoint and compare hashes)")
     return p.parse_args()
@@ -202,8 +203,11 @@ def _handle_run(args, W, H, boundary, devices, transport):
             b.set_option("transport", 2)  # raises when RCCL cannot serve this placement
         k = b.parts()[0]["ghost"] if parts > 1 else b.info()["tblock_k"]
         b.seed_splitmix(args.seed)
-        b.step(args.warmup * k)
+        # warm up to the main leg's first timed generation: the same window of the same board (the launch time drifts
+        # with the board's activity and the clock)
+        b.step(max(args.warmup * k, args.handle_first_gen))
         b.synchronize()
+        first = b.generation
         t0 = time.perf_counter()
         dev_us = b.step_timed(args.steps * k)
         dt = time.perf_counter() - t0
@@ -215,6 +219,7 @@ def _handle_run(args, W, H, boundary, devices, transport):
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "avg_pass_us_device_events": round(dev_us / args.steps, 2),
             "generations_per_step": k,
+            "first_generation_timed": first,
             "transport": b.transport(),
         }
         if timing is not None:
@@ -254,13 +259,14 @@ def handle_leg(args, W, H, boundary, parts, ndev):
     return out
 
 
-def run_handle_leg(args, W, H, boundary, parts, verify_gen):
+def run_handle_leg(args, W, H, boundary, parts, verify_gen, first_gen=0):
     """The handle leg in a child process of rank 0 under a time limit: it may create an RCCL communicator over all
     GPUs inside one process, and a failure or hang there must not cost the main line.  The child never imports
     torch (bench.py main)."""
     cmd = [sys.executable, os.path.abspath(__file__), "--handle-leg-child", "--width", str(W), "--height", str(H),
            "--boundary", args.boundary, "--handle-parts", str(parts), "--steps", str(args.steps),
-           "--warmup", str(args.warmup), "--seed", str(args.seed), "--verify-gen", str(verify_gen)]
+           "--warmup", str(args.warmup), "--seed", str(args.seed), "--verify-gen", str(verify_gen),
+           "--handle-first-gen", str(first_gen)]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
@@ -560,7 +566,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier(group=host_group)
         if rank == 0:
-            handle = run_handle_leg(args, W, H, boundary, parts, verify_gen)
+            handle = run_handle_leg(args, W, H, boundary, parts, verify_gen, first_gen)
         if world > 1:
             dist.barrier(group=host_group)
     if rank == 0 and got_hash is not None:
