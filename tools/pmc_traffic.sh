@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 out=gpurun_out/pmc_traffic_${boundary}_k$k
 mkdir -p $out
 steps=8
-bench="python3 bench.py --no-cpu-baseline --steps $steps --warmup 1 --tblock $k --boundary $boundary"
+bench="python3 bench.py --no-cpu-baseline --no-verify --handle-parts 0 --steps $steps --warmup 1 --tblock $k --boundary $boundary"
 calib=tools/ubench/traffic_calib
 [ -x $calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o $calib tools/ubench/traffic_calib.hip
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/calib_fetch -o run -- $calib > $out/calib_fetch.log 2>&1
