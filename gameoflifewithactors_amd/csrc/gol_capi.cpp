@@ -228,6 +228,9 @@ struct BoardOptions {
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
     int resident_threads = 1024;              // "resident_threads": LDS-resident workgroup size (1024 or 256)
+    bool lanes = false;                       // "lanes": rows-on-lanes band pass (gol_lanes.hip) where it applies,
+                                              // in place of the cooperative pass, for calls of >= 2 * coop depth
+    int lanes_m = 0;                          // "lanes_m": its words per lane and half-row (0 = by width, 5, 9, 17)
 };
 
 struct gol_board {
@@ -250,6 +253,7 @@ struct gol_board {
     uint32_t* coop_xch = nullptr;       // cooperative pass: hand-off granules (allocated on first use)
     int64_t coop_xch_words = 0;
     unsigned coop_epoch = 0;            // tag epoch of the last cooperative launch (1..65535)
+    int64_t lanes_launches = 0;         // launches of the rows-on-lanes pass on this board (option "lanes_launches")
     uint32_t* rag[2] = {nullptr, nullptr};  // ragged byte boards on the cooperative pass: whole-word scratch rows
     int64_t rag_words = 0;                  // capacity of each rag buffer
     // Ragged byte boards between gol_step calls of the multi-generation passes keep their state in the scratch rows:
@@ -452,6 +456,16 @@ int coop_depth(const gol_board* b) {
     return b->tblock < gol::kCoopDefaultK ? b->tblock : gol::kCoopDefaultK;
 }
 
+// The rows-on-lanes band pass (gol_lanes.hip) on a packed single board, for a call of `gens` generations: the boards
+// the cooperative pass would take whose width splits into windows (64 (m - 1) columns each), calls of at least two
+// hand-off blocks (the pass stages the board through LDS at both ends of a launch).
+bool use_lanes(const gol_board* b, int64_t gens) {
+    if (!b->opt.lanes || !b->opt.coop || !b->packed || b->multi) return false;
+    gol::LanesPlan p;
+    return gens >= 2 * coop_depth(b) && b->W * b->H <= b->opt.coop_max_cells &&
+           gol::lanes_plan(b->W, b->H, coop_depth(b), b->opt.lanes_m, &p);
+}
+
 bool use_coop(const gol_board* b) {
     if (!b->opt.coop || !b->packed) return false;
     const int cm = gol::coop_m(b->W / 32);
@@ -485,15 +499,22 @@ bool use_coop_ragged(const gol_board* b, int64_t* pitch) {
 // scratch rows of a ragged board of that width), ping-ponging between bufs[*cur] and bufs[*cur ^ 1]; *cur ends on
 // the result.  One launch per kCoopMaxGensPerLaunch generations.
 int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w, uint32_t* const bufs[2], int* cur,
-               int64_t gens) {
+               int64_t gens, bool lanes = false) {
     if (!b->coop) {
         GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
         GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
     }
     int nwg = 0, B = 0, R = 0;
     const int k = coop_depth(b);
-    (void)gol::coop_plan(W, b->H, k, &nwg, &B, &R, b->opt.coop_r);
-    const int64_t need = gol::coop_xch_words(W, nwg, k);
+    int64_t need = 0;
+    if (lanes) {
+        gol::LanesPlan lp;
+        (void)gol::lanes_plan(W, b->H, k, b->opt.lanes_m, &lp);
+        need = gol::lanes_xch_words(lp, k);
+    } else {
+        (void)gol::coop_plan(W, b->H, k, &nwg, &B, &R, b->opt.coop_r);
+        need = gol::coop_xch_words(W, nwg, k);
+    }
     if (need > b->coop_xch_words) {
         if (b->coop_xch) {
             GOL_HIP(hipStreamSynchronize(b->stream));
@@ -515,9 +536,17 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
             GOL_HIP(hipMemsetAsync(b->coop_xch, 0, (size_t)b->coop_xch_words * sizeof(uint32_t), b->stream));
             b->coop_epoch = 1;
         }
-        GOL_HIP(gol::launch_coop_pass(bufs[*cur], bufs[*cur ^ 1], W, b->H, pitch, ilv, k, g, b->boundary == GOL_BOUNDED,
-                                      b->coop_epoch, reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
-                                      b->coop_xch_words, b->stream, ragged_w, tune));
+        if (lanes) ++b->lanes_launches;
+        if (lanes)
+            GOL_HIP(gol::launch_lanes_pass(bufs[*cur], bufs[*cur ^ 1], W, b->H, pitch, ilv, k, g,
+                                           b->boundary == GOL_BOUNDED, b->coop_epoch,
+                                           reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
+                                           b->coop_xch_words, b->stream, b->opt.lanes_m, tune));
+        else
+            GOL_HIP(gol::launch_coop_pass(bufs[*cur], bufs[*cur ^ 1], W, b->H, pitch, ilv, k, g,
+                                          b->boundary == GOL_BOUNDED, b->coop_epoch,
+                                          reinterpret_cast<int*>(b->coop + kCoopErrWord), b->coop_xch,
+                                          b->coop_xch_words, b->stream, ragged_w, tune));
         *cur ^= 1;
         b->generation += g;
         gens -= g;
@@ -589,6 +618,10 @@ int step_impl(gol_board* b, int64_t gens) {
             gens -= g;
         }
         return GOL_OK;
+    }
+    if (use_lanes(b, gens)) {
+        uint32_t* bufs[2] = {b->words(0), b->words(1)};
+        return coop_steps(b, b->W, b->pitch, b->ilv, 0, bufs, &b->cur, gens, true);
     }
     if (use_coop(b)) {
         uint32_t* bufs[2] = {b->words(0), b->words(1)};
@@ -1372,6 +1405,11 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (value < 0 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be 0..4096");
         o.coop_poll_delay = (int)value;
     } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
+    else if (n == "lanes") o.lanes = value != 0;
+    else if (n == "lanes_m") {
+        if (value != 0 && value != 5 && value != 9 && value != 17) return fail(GOL_ERR_INVALID, "lanes_m must be 0, 5, 9 or 17");
+        o.lanes_m = (int)value;
+    }
     else if (n == "resident_threads") {
         if (value != 256 && value != 1024) return fail(GOL_ERR_INVALID, "resident_threads must be 256 or 1024");
         o.resident_threads = (int)value;
@@ -1406,6 +1444,9 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "coop_r") *value = o.coop_r;
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
     else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
+    else if (n == "lanes") *value = o.lanes;
+    else if (n == "lanes_m") *value = o.lanes_m;
+    else if (n == "lanes_launches") *value = b->lanes_launches;
     else if (n == "resident_threads") *value = o.resident_threads;
     else if (n == "coop_epoch") *value = b->coop_epoch;
     else if (n == "transport") *value = b->multi ? b->multi->transport() : GOL_TRANSPORT_NONE;

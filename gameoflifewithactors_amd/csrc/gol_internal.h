@@ -122,6 +122,22 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
                             hipStream_t s, int64_t ragged_w = 0, const CoopTuning& tune = CoopTuning());
 
+// ---- gol_lanes.hip: rows-on-lanes band pass (a wave owns all rows of a band window of 64 (m - 1) columns and
+// steps it k generations alone), packed boards of any interleave, W a multiple of 64 (m - 1), k <= 16
+struct LanesPlan {
+    int m = 0;     // words per lane and half-row (5, 9 or 17)
+    int nx = 0;    // windows per band (waves per workgroup)
+    int nb = 0;    // bands (workgroups)
+    int bmax = 0;  // rows of the tallest band
+};
+// m_opt: 0 = by width (9 when W % 512 == 0, else 5), or 5 / 9 / 17
+bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out);
+int64_t lanes_xch_words(const LanesPlan& p, int k);
+// as launch_coop_pass (gens <= 65535 per launch, epoch-tagged granules in xch, *err on a timed-out wait)
+hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
+                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
+                             hipStream_t s, int m_opt, const CoopTuning& tune);
+
 // ---- gol_wave.hip: whole board in one wavefront's registers (W <= 128, H <= 256), all generations in one launch
 int wave_resident_rpl(int64_t W, int64_t H);  // rows per lane, 0 = the board does not fit
 hipError_t launch_wave_resident(const void* src, void* dst, int64_t W, int64_t H, int64_t pitch, int64_t gens,
