@@ -10,6 +10,8 @@ step() {  # step NAME SECONDS CMD...
   if [ $rc -ge 124 ]; then tail -20 $O/$name.log; echo "stopping after $name (rc $rc)"; exit $rc; fi
   return 0
 }
+step lanes_ab 300 python tools/lanes_ab.py --rounds 3
+grep '^{' $O/lanes_ab.log | cut -c1-150
 step bench_n1_a 300 python bench.py --gpus 1 --steps 20 --warmup 5
 grep -o '"value": [0-9.]*\|"verify": {[^}]*}\|"avg_launch_us": [0-9.]*\|"value_device_events": [0-9.]*\|"first_generation_timed": [0-9]*' $O/bench_n1_a.log | tr '\n' ' '; echo
 for split in 0.66 0.70 0.74 0.62 0.68 0.72; do
