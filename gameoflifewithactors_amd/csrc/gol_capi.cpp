@@ -221,9 +221,10 @@ struct BoardOptions {
     int seam = 0;                             // "seam": torus seam strips (0 = where they apply, -1 = off)
     bool ragged_stream = true;                // "ragged_stream": ragged boards beyond the cooperative pass stream
                                               // packed words (0: the per-generation byte step)
-    bool ragged_ring = true;                  // "ragged_ring": ragged boards stream as block rows (torus: ring rows on
+    int ragged_ring = 1;                      // "ragged_ring": ragged boards stream as block rows (torus: ring rows on
                                               // the aligned kernel; bounded: column-masked block rows) in the aligned
-                                              // layouts (0: ilv-1 rows, bit-level row ends on a torus)
+                                              // layouts: 1 from kRingMinCells cells, 2 always, 0 never (ilv-1 rows,
+                                              // bit-level row ends on a torus)
     int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
@@ -590,7 +591,14 @@ bool use_stream_ragged(const gol_board* b) {
 // copies rewritten after every pass.  Bounded: rows of ceil(W / 64) blocks, the last one partial, on edge-fill strips
 // that AND per-word column masks at every level (gol_step.hip NARROW = 2).  Layout and depth follow the aligned rules
 // for a board of that many cells (board_ilv / board_tblock): ilv 2 from 2^25 cells, K = 16 below 2^29, 12 above.
-bool use_ring(const gol_board* b) { return b->opt.ragged_ring; }
+// Block rows beat the ilv-1 rows from about 2^27.6 cells (profiles/r4/ragged_ab_b.log, us/generation, torus /
+// bounded): 65535^2 41-43 vs 60 / 44-47 vs 52-54, 16383^2 5.2 vs 6.0 / 5.7 vs 5.6; below they lose: 8193 x 20000 5.0
+// vs 4.7 / 4.9 vs 4.5, 10001^2 4.7 vs 3.6 / 4.6 vs 3.4.  Option "ragged_ring": 1 = by this size, 2 = always, 0 = never.
+constexpr int64_t kRingMinCells = (int64_t)3 << 26;
+bool ring_by_size(int64_t W, int64_t H) { return W * H >= kRingMinCells; }
+bool use_ring(const gol_board* b) {
+    return b->opt.ragged_ring == 2 || (b->opt.ragged_ring == 1 && ring_by_size(b->W, b->H));
+}
 constexpr int kRingCopy = 64;  // cells copied at each end of a ring row (gol_formats.hip kRingPad; the suffix has >= 64)
 int64_t ring_cells(int64_t W, int64_t H, int boundary) { return gol::ring_pitch(W, boundary == GOL_TORUS) * 32 * H; }
 int ring_ilv(const gol_board* b) { return ring_cells(b->W, b->H, b->boundary) < kSmallBoardCells ? 1 : 2; }
@@ -934,8 +942,8 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->packed = (width % 32) == 0;
         b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n)) : 0;
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
-        if (!b->packed && !tblock_k) {
-            // ragged boards stream as block rows of ring_pitch(W) words: the aligned rules for that many cells
+        if (!b->packed && !tblock_k && ring_by_size(width, height)) {
+            // large ragged boards stream as block rows of ring_pitch(W) words: the aligned rules for that many cells
             const int64_t rc = ring_cells(width, height, boundary);
             b->tblock = board_tblock(rc < kSmallBoardCells ? 1 : 2, rc, boundary);
         }
@@ -1397,7 +1405,10 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         return b->multi->set_transport((int)value);
     }
     else if (n == "ragged_stream") o.ragged_stream = value != 0;
-    else if (n == "ragged_ring") o.ragged_ring = value != 0;
+    else if (n == "ragged_ring") {
+        if (value < 0 || value > 2) return fail(GOL_ERR_INVALID, "ragged_ring must be 0, 1 (by size) or 2");
+        o.ragged_ring = (int)value;
+    }
     else if (n == "coop_r") {
         if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
         o.coop_r = (int)value;

@@ -64,9 +64,11 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *             packed boards from 2^29 cells, width % 64 == 0: ilv 2, k = 12 -- torus and bounded alike
  *               (bounded boards ran k = 16 until round 3), single board or strips;
  *             other packed widths from 2^25 cells: ilv 1, k = 32;
- *             byte boards (width % 32 != 0, ilv 0): the rules above for the block rows they stream as (DESIGN.md
- *               4.1 "Ragged rows": 2 * ceil((W + 128) / 64) words per ring row on a torus, 2 * ceil(W / 64) when
- *               bounded; ilv 1 k = 8 below 2^25 of those cells, ilv 2 k = 16 below 2^29, k = 12 above);
+ *             byte boards (width % 32 != 0, ilv 0) below 3 * 2^26 cells: k = 8 below 2^25 cells, 16 below 2^27,
+ *               24 above (the ilv-1 scratch rows they stream as);
+ *             byte boards from 3 * 2^26 cells: the rules above for the block rows they stream as (DESIGN.md 4.1
+ *               "Ragged rows": 2 * ceil((W + 128) / 64) words per ring row on a torus, 2 * ceil(W / 64) when
+ *               bounded; ilv 2 k = 16 below 2^29 of those cells, k = 12 above);
  *           else one of 1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k.
  *           A multi-part board's halo depth (gol_part_info ghost) is the deepest supported k <= tblock_k that
  *           fits its thinnest strip.
@@ -176,8 +178,9 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *   "transport" 1 | 2            multi-part boards: halo rows by peer copies (1) or RCCL (2, distinct devices;
  *                                GOL_ERR_UNSUPPORTED otherwise); GOL_ERR_UNSUPPORTED on a single board
  *   ("split", "seg_rows" and "seam" apply to every strip launch of a multi-part board as well)
- *   "ragged_ring" 1 | 0          ragged boards on the streaming pass as block rows in the aligned layouts (torus: ring
- *                                rows; bounded: column-masked rows; 0: ilv-1 rows)
+ *   "ragged_ring" 1 | 2 | 0      ragged boards on the streaming pass as block rows in the aligned layouts (torus: ring
+ *                                rows; bounded: column-masked rows) from 3 * 2^26 cells (1), on every size (2), or
+ *                                never (0: ilv-1 rows)
  *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
  *                                words (0: the per-generation byte step)
  *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments

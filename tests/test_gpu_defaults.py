@@ -18,13 +18,15 @@ def gol():
 
 # (width, height, boundary) -> (packed, ilv, tblock_k), the table in gol.h
 CASES = [
-    ((100, 100, 0), (False, 0, 8)),          # the reference's own board: byte board, ring rows below 2^25 cells
-    ((10001, 10001, 0), (False, 0, 16)),     # byte torus board: ring rows of 2^25 .. 2^29 cells, k 16
-    ((20001, 10001, 0), (False, 0, 16)),
-    ((65535, 8193, 0), (False, 0, 12)),      # ... from 2^29 ring cells, k 12
-    ((10001, 10001, 1), (False, 0, 16)),     # bounded byte board: block rows of 2^25 .. 2^29 cells, k 16
-    ((20001, 10001, 1), (False, 0, 16)),
-    ((65535, 8193, 1), (False, 0, 12)),      # ... from 2^29, k 12
+    ((100, 100, 0), (False, 0, 8)),          # the reference's own board: byte board, ilv-1 rows below 2^25 cells, k 8
+    ((10001, 10001, 0), (False, 0, 16)),     # byte boards below 3 * 2^26 cells: ilv-1 rows, k 16 below 2^27 ...
+    ((20001, 10001, 0), (False, 0, 24)),     # ... k 24 above
+    ((65535, 8193, 0), (False, 0, 12)),      # from 3 * 2^26 cells: ring rows, the aligned rules (k 12 from 2^29)
+    ((30001, 10001, 0), (False, 0, 16)),     # ... k 16 below 2^29 ring cells
+    ((10001, 10001, 1), (False, 0, 16)),     # bounded: the same classes (block rows from 3 * 2^26 cells)
+    ((20001, 10001, 1), (False, 0, 24)),
+    ((30001, 10001, 1), (False, 0, 16)),
+    ((65535, 8193, 1), (False, 0, 12)),
     ((1024, 1024, 0), (True, 1, 8)),         # packed below 2^25, not a cooperative-pass width: ilv 1, k 8
     ((4096, 4096, 0), (True, 2, 16)),        # cooperative-pass board 4096 wide: ilv 2, k 16
     ((8192, 8192, 1), (True, 4, 8)),         # cooperative-pass board 8192 wide: ilv 4, k 8

@@ -1,6 +1,7 @@
 """GPU parity of ragged boards on the streaming pass (torus: ring rows on the aligned kernel, gol_formats.hip
-gol_pack_ring / gol_ring_refresh, or with the board option "ragged_ring" 0 the M = 1 kRagged variant of
-csrc/gol_step.hip; bounded: the column-masked variant; DESIGN.md 4.1 "Ragged rows").
+gol_pack_ring / gol_ring_refresh; bounded: column-masked block rows) from 3 * 2^26 cells (board option "ragged_ring"
+1, the default; 2 forces them on any size, as these tests do), below that the M = 1 kRagged variant of
+csrc/gol_step.hip ("ragged_ring" 0 everywhere; DESIGN.md 4.1 "Ragged rows").
 
 The reference's board size is any integer (GameOfLifeLogic.fs:5, GameofLife.fs:18).  Byte boards whose width is not
 a multiple of 32 and that the cooperative pass does not take (wider than 8192 cells or above 2^26 cells) run the
@@ -44,7 +45,7 @@ def _run(gol, b0, boundary, steps, stream, tblock_k=0, ring=1):
 WIDTHS = [8193, 8209, 8223, 10001, 62 * 133 * 32 - 31, 62 * 134 * 32 + 5, 16383]
 
 
-@pytest.mark.parametrize("boundary,ring", [(0, 1), (0, 0), (1, 1), (1, 0)])
+@pytest.mark.parametrize("boundary,ring", [(0, 2), (0, 0), (1, 2), (1, 0), (0, 1)])
 @pytest.mark.parametrize("w", WIDTHS)
 def test_ragged_stream_matches_oracle(gol, oracle, w, boundary, ring):
     h = 70
@@ -63,7 +64,7 @@ def test_ragged_ring_interleaved(gol, oracle, w, boundary):
     block is partial (1 .. 63 of its cells on the board), masked at every level (gol_step.hip NARROW = 2)."""
     h = (1 << 25) // w + 40
     b0 = _rand(h, w, w, p=0.3)
-    with gol.Board(w, h, boundary, options={"coop": 0}) as b:
+    with gol.Board(w, h, boundary, options={"coop": 0, "ragged_ring": 2}) as b:  # below the size rule: forced
         assert b.info()["tblock_k"] == 16
         b.set_cells(b0).step(16 + 12 + 5)
         got_rows = b.get_region(0, 0, w, 64)

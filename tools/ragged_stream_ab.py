@@ -1,6 +1,7 @@
 """Ragged boards past the cooperative pass (width not a multiple of 32, wider than 8192 or above 2^26 cells), passes
-interleaved on one box: block rows in the aligned layouts (board option ragged_ring=1, the default: ring rows on a
-torus, column-masked rows when bounded), the ilv-1 rows (ragged_ring=0), and optionally the per-generation byte step
+interleaved on one box: block rows in the aligned layouts (board option ragged_ring=2: ring rows on a torus,
+column-masked rows when bounded), the ilv-1 rows (ragged_ring=0), the default choice by size (auto, ragged_ring=1),
+and optionally the per-generation byte step
 (ragged_stream=0).  Timing: the
 library's own HIP events around one gol_step call (gol_step_timed; no torch in the process), after 40 warm-up
 generations; the state stays in the scratch rows between the calls (DESIGN.md 4.1 "Ragged rows").  One JSON line per
@@ -18,7 +19,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 BOARDS = "10001x10001x192,16383x16383x96,8193x20000x192,65535x65535x48"
-OPTS = {"ring": {"ragged_stream": 1, "ragged_ring": 1}, "m1": {"ragged_stream": 1, "ragged_ring": 0},
+OPTS = {"ring": {"ragged_stream": 1, "ragged_ring": 2}, "m1": {"ragged_stream": 1, "ragged_ring": 0},
+        "auto": {"ragged_stream": 1, "ragged_ring": 1},
         "bytestep": {"ragged_stream": 0}}
 
 
