@@ -408,7 +408,20 @@ hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int6
     a.poll_delay = tune.poll_delay >= 0 ? tune.poll_delay : 8;
     a.spin_limit = tune.spin_limit ? tune.spin_limit : kLaneSpinLimit;
     a.err = err;
-    const size_t lds = ((size_t)kWinRows * a.nw + (size_t)2 * p.nx * 64) * sizeof(uint32_t);
+    size_t lds = ((size_t)kWinRows * a.nw + (size_t)2 * p.nx * 64) * sizeof(uint32_t);
+    // spread the bands evenly: an LDS request that admits at most ceil(nb / CUs) workgroups per CU (the dispatcher
+    // would otherwise stack two bands on one CU while another idles, and every band waits on the slowest)
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 0;
+        return n;
+    }();
+    if (cus > 0) {
+        const size_t per_cu = ((size_t)p.nb + cus - 1) / cus;
+        const size_t floor = (size_t)160 * 1024 / (per_cu + 1) + 1024;
+        if (floor * per_cu <= (size_t)160 * 1024 && floor > lds) lds = floor;
+    }
     {  // the LDS attribute once per kernel
         static std::mutex mu;
         static std::vector<const void*> done;
