@@ -3,7 +3,7 @@
 # again with no torch in the process (gpurun_out/r4b/bench_c2.log).  Each probe prints its exit code.
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r4d; mkdir -p $O
+O=$R/gpurun_out/r4f/exit; mkdir -p $O
 P="import sys; sys.path.insert(0, '$R'); from gameoflifewithactors_amd import _lib, Board; _lib.load()"
 probe() {  # probe NAME PYCODE [under-profiler]
   if [ "$3" = prof ]; then
