@@ -26,3 +26,7 @@ with Board(4096, 4096, 0) as b: b.seed_splitmix(1).step(100); b.synchronize()
 sys.stdout.flush(); os._exit(0)" prof
 probe torch_then_coop_prof "import torch; $P
 with Board(4096, 4096, 0) as b: b.seed_splitmix(1).step(100); b.synchronize()" prof
+# the smallest hipcc library with one kernel (not libgol_hip.so): built here, loaded by ctypes
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -shared -fPIC -o $O/libtiny.so $R/tools/diag/tiny.hip && \
+probe tiny_lib_prof "import ctypes; l = ctypes.CDLL('$O/libtiny.so'); print('tiny', l.tiny_run())" prof
+probe tiny_lib_noprof "import ctypes; l = ctypes.CDLL('$O/libtiny.so'); print('tiny', l.tiny_run())"
