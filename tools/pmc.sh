@@ -14,5 +14,7 @@ G[3]="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_W
 G[4]="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 G[5]="TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum"  # at most 4 TCC counters per pass
 for i in $groups; do
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$i]} --output-format csv -d $out/g$i -o run -- $cmd > $out/g$i.log 2>&1 || { echo "group $i failed rc=$?"; tail -3 $out/g$i.log; }
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$i]} --output-format csv -d $out/g$i -o run -- $cmd > $out/g$i.log 2>&1
+  rc=$?
+  if [ $rc -ne 0 ]; then echo "group $i failed rc=$rc"; tail -3 $out/g$i.log; exit $rc; fi  # nothing more on the GPU
 done

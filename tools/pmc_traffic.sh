@@ -13,9 +13,13 @@ bench="python3 bench.py --no-cpu-baseline --no-verify --handle-parts 0 --steps $
 calib=tools/ubench/traffic_calib
 [ -x $calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o $calib tools/ubench/traffic_calib.hip
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/calib_fetch -o run -- $calib > $out/calib_fetch.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "pass failed rc=$rc: $(tail -2 $out/calib_fetch.log)"; exit $rc; }
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/calib_write -o run -- $calib > $out/calib_write.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "pass failed rc=$rc: $(tail -2 $out/calib_write.log)"; exit $rc; }
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $out/bench_fetch -o run -- $bench > $out/bench_fetch.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "pass failed rc=$rc: $(tail -2 $out/bench_fetch.log)"; exit $rc; }
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $out/bench_write -o run -- $bench > $out/bench_write.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "pass failed rc=$rc: $(tail -2 $out/bench_write.log)"; exit $rc; }
 merge=gpurun_out/pmc_traffic/pmc_traffic.json
 mkdir -p gpurun_out/pmc_traffic
 [ -f $merge ] || cp profiles/pmc_traffic.json $merge
