@@ -261,6 +261,20 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+def unload() -> None:
+    """dlclose libgol_hip.so now, while the HIP runtime -- and a profiler attached to it -- is still alive, so its
+    device code is unregistered here and not in the process-exit destructors (DESIGN.md 6 "Exit under rocprofv3").
+    Close every board first.  load() maps it again afterwards."""
+    global _lib
+    if _lib is None:
+        return
+    import _ctypes
+
+    handle = _lib._handle
+    _lib = None
+    _ctypes.dlclose(handle)
+
+
 def device_count() -> int:
     """HIP devices visible to the library (gol_device_count; no torch needed)."""
     n = ctypes.c_int()

@@ -13,9 +13,16 @@ probe() {  # probe NAME PYCODE: under rocprofv3 --kernel-trace --stats; stops th
   echo "$1 rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $O/$1.log; exit $rc; fi
 }
-# 1. the smallest hipcc library with one kernel (not libgol_hip.so), loaded by ctypes
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -shared -fPIC -o $O/libtiny.so $R/tools/diag/tiny.hip || exit 1
-probe tiny_lib "import ctypes; l = ctypes.CDLL('$O/libtiny.so'); print('tiny', l.tiny_run())"
+T="import ctypes, _ctypes; l = ctypes.CDLL('$O/libtiny.so'); print('tiny', l.tiny_run())"
+# 0. dlclose before exit (the library's device code unregistered while the profiler is alive): expected clean
+probe tiny_lib_dlclose "$T
+_ctypes.dlclose(l._handle)"
+probe coop_board_unload "$P
+with Board(4096, 4096, 0) as b: b.seed_splitmix(1).step(100); b.synchronize()
+_lib.unload()"
+# 1. the smallest hipcc library with one kernel (not libgol_hip.so), loaded by ctypes
+probe tiny_lib "$T"
 # 2. libgol_hip.so loaded, no board
 probe load_only "$P"
 # 3. a streaming board
