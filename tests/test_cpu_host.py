@@ -59,6 +59,22 @@ def test_library_reports_version_without_gpu():
     assert b"gfx950" in _lib.load().gol_version()
 
 
+def test_library_unloads_and_reloads():
+    """_lib.unload() dlcloses the library (its device code unregistered before process exit); load()
+    maps it again.  In a child process: other tests hold the loaded library."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gameoflifewithactors_amd import _lib\n"
+            "_lib.load(); _lib.unload(); assert _lib._lib is None\n"
+            "print(_lib.load().gol_version().decode()); _lib.unload()\n") % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "gfx950" in r.stdout
+
+
 def test_arch_check_accepts_only_gfx950():
     """gol_create refuses a board on a non-gfx950 device with GOL_ERR_NO_DEVICE (gol.h): the check's
     decision on the device's gcnArchName, host code, exercised without a GPU."""
