@@ -65,4 +65,5 @@ def test_torch_first_shares_torchs_runtime_and_library_alone_runs_on_rocm():
 def test_torch_after_the_library_warns():
     out = _run([_BOARD, _TORCH_LATE])
     assert any("import torch before" in m for m in out["late_torch"]), out
-    assert len(out["runtimes"]) == 1, out
+    # what the warning is about: torch then maps its own runtime beside the library's (two are mapped now)
+    assert len(out["runtimes"]) == 2 and any("/torch/" not in r for r in out["runtimes"]), out

@@ -5,7 +5,7 @@
 # GPU work of the call).  Each prints its exit code.
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r4f/exit; mkdir -p $O
+O=$R/gpurun_out/r4h/exit; mkdir -p $O
 P="import sys; sys.path.insert(0, '$R'); from gameoflifewithactors_amd import _lib, Board; _lib.load()"
 probe() {  # probe NAME PYCODE: under rocprofv3 --kernel-trace --stats; stops the script unless it exits 0
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$1 -o run -- python3 -c "$2" > $O/$1.log 2>&1
