@@ -36,7 +36,7 @@ def _rand(h, w, seed, p=0.45):
 
 def _run(gol, b0, boundary, steps, coop, k=None, ilv=0):
     h, w = b0.shape
-    opts = {"coop": int(coop)}
+    opts = {"coop": int(coop), "lanes": 0}
     if k:
         opts["coop_k"] = k
     with gol.Board(w, h, boundary, ilv=ilv, options=opts) as b:
@@ -80,7 +80,7 @@ def test_coop_config2_golden_checkpoints(gol):
     population every 100 generations) to generation 10,000, on the cooperative pass."""
     with open(os.path.join(HERE, "golden", "golden_long.json")) as f:
         case = json.load(f)["c2_4096_torus_dotnet42"]
-    with gol.Board(case["width"], case["height"], case["boundary"], options={"coop": 1}) as b:
+    with gol.Board(case["width"], case["height"], case["boundary"], options={"coop": 1, "lanes": 0}) as b:
         b.seed_dotnet(case["seed"], gol.INIT_DOTNET_MOD2)
         done = 0
         for gen, h, pop in case["checkpoints"]:
@@ -93,7 +93,7 @@ def test_coop_epoch_wrap(gol, oracle):
     """The hand-off granules carry a 16-bit launch epoch; at the wrap the host clears them. Launches just before,
     at and after the wrap (the "coop_epoch" option sets the epoch of the last launch) must stay exact."""
     b0 = _rand(1024, 1024, 77)
-    with gol.Board(1024, 1024, 0, options={"coop": 1}) as b:
+    with gol.Board(1024, 1024, 0, options={"coop": 1, "lanes": 0}) as b:
         b.set_cells(b0)
         b.step(9)  # first launch: allocates and clears the exchange buffer
         done = 9
@@ -112,7 +112,7 @@ def test_coop_timeout_reported_on_every_readback(gol, oracle):
     launch must still end (no further waits once one has failed), and the board must be usable again once it is
     overwritten."""
     b0 = _rand(2048, 2048, 91)
-    with gol.Board(2048, 2048, 0, options={"coop": 1, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
+    with gol.Board(2048, 2048, 0, options={"coop": 1, "lanes": 0, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
         b.set_cells(b0)
         failed = False
         for _ in range(20):  # the race is lost almost always at once; a few tries make it certain
@@ -138,7 +138,7 @@ def test_coop_timeout_then_overwrite_without_readback(gol, oracle):
     overwrite: the overwrite must succeed (the stale error word is cleared without marking the board invalid) and
     the board must read back valid and exact."""
     b0 = _rand(2048, 2048, 92)
-    with gol.Board(2048, 2048, 0, options={"coop": 1, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
+    with gol.Board(2048, 2048, 0, options={"coop": 1, "lanes": 0, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
         b.set_cells(b0)
         for _ in range(5):  # nothing reads the error word in between
             b.step(200)
@@ -166,7 +166,7 @@ def test_coop_ragged_widths(gol, oracle, w, h, boundary):
     steps = [16, 3, 21]  # 3 < 16: the byte step between two pass calls
     want = oracle.c_run(b0, sum(steps), boundary)
     for coop in (True, False):
-        with gol.Board(w, h, boundary, options={"coop": int(coop)}) as b:
+        with gol.Board(w, h, boundary, options={"coop": int(coop), "lanes": 0}) as b:
             assert not b.info()["packed"]
             b.set_cells(b0)
             for g in steps:
@@ -179,7 +179,7 @@ def test_coop_ragged_byte_values(gol, oracle):
     """Byte cells are alive when nonzero (any value); the ragged pass writes the board back as 0 / 1."""
     b0 = _rand(200, 1001, 5)
     vals = (b0 * np.random.default_rng(6).integers(1, 256, size=b0.shape)).astype(np.uint8)
-    with gol.Board(1001, 200, 0, options={"coop": 1}) as b:
+    with gol.Board(1001, 200, 0, options={"coop": 1, "lanes": 0}) as b:
         b.set_cells(vals)
         b.step(24)
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 24, 0))
