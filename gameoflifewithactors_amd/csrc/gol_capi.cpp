@@ -232,6 +232,8 @@ struct BoardOptions {
     bool lanes = false;                       // "lanes": rows-on-lanes band pass (gol_lanes.hip) where it applies,
                                               // in place of the cooperative pass, for calls of >= 2 * coop depth
     int lanes_m = 0;                          // "lanes_m": its words per lane and half-row (0 = by width, 5, 9, 17)
+    bool coop_launch = true;                  // "coop_launch": persistent passes by hipLaunchCooperativeKernel (0:
+                                              // hipLaunchKernel; their grids fit the device by construction)
 };
 
 struct gol_board {
@@ -531,6 +533,7 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     tune.min_rows = b->opt.coop_r;
     tune.poll_delay = b->opt.coop_poll_delay;
     tune.spin_limit = (unsigned)std::min<int64_t>(b->opt.coop_spin_limit, 0xffffffffLL);
+    tune.plain_launch = !b->opt.coop_launch;
     while (gens > 0) {
         const int64_t g = gens < kCoopMaxGensPerLaunch ? gens : kCoopMaxGensPerLaunch;
         if (++b->coop_epoch > 0xffff) {  // tags of an earlier epoch could match again: clear the granules
@@ -1417,6 +1420,7 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         o.coop_poll_delay = (int)value;
     } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
     else if (n == "lanes") o.lanes = value != 0;
+    else if (n == "coop_launch") o.coop_launch = value != 0;
     else if (n == "lanes_m") {
         if (value != 0 && value != 5 && value != 9 && value != 17) return fail(GOL_ERR_INVALID, "lanes_m must be 0, 5, 9 or 17");
         o.lanes_m = (int)value;
@@ -1456,6 +1460,7 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
     else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
     else if (n == "lanes") *value = o.lanes;
+    else if (n == "coop_launch") *value = o.coop_launch;
     else if (n == "lanes_m") *value = o.lanes_m;
     else if (n == "lanes_launches") *value = b->lanes_launches;
     else if (n == "resident_threads") *value = o.resident_threads;

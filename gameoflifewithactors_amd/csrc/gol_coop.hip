@@ -568,6 +568,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
         }
     }
     void* args[] = {&a};
+    if (tune.plain_launch) return hipLaunchKernel(fn, dim3(nwg), dim3(kThreads), args, lds, s);
     return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);
 }
 

@@ -117,6 +117,7 @@ struct CoopTuning {
     int min_rows = 1;
     int poll_delay = 8;
     unsigned spin_limit = 0;
+    bool plain_launch = false;  // hipLaunchKernel instead of hipLaunchCooperativeKernel (the grid fits by construction)
 };
 hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,

@@ -43,7 +43,7 @@ constexpr unsigned kLaneSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means 
 struct LaneArgs {
     const uint32_t* src;  // board at launch
     uint32_t* dst;        // board after `gens` generations
-    uint64_t* xch;        // granules: [2 parity][nb][2 (top, bottom)][K][nx][2 halves][M] {word, tag}
+    uint64_t* xch;        // granules: [2 parity][nb][2 (top, bottom)][nx][M][2 halves][K rows] {word, tag}
     int64_t pitch;        // words per board row
     int nw;               // words per row (W / 32)
     int ilv;              // the board's interleave (1, 2, 4)
@@ -131,17 +131,21 @@ __device__ void stage_out(const LaneArgs& a, const uint32_t* rows, int first, in
     }
 }
 
+// A lane's M granules sit `stride` granules apart: word t of every publishing lane of a window side is one contiguous
+// run (lanes of consecutive rows at consecutive granules), so each store / poll instruction touches two short runs
+// instead of 64 lanes 8 M bytes apart.
 template <int M>
-__device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M], unsigned tag) {
+__device__ __forceinline__ void st_granules(uint64_t* p, int stride, const uint32_t (&w)[M], unsigned tag) {
 #pragma unroll
     for (int t = 0; t < M; t++)
-        __hip_atomic_store(p + t, (uint64_t)tag << 32 | w[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + (int64_t)t * stride, (uint64_t)tag << 32 | w[t], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The lane's M granules (src == nullptr: the lane needs none), in one batch of 8-byte sc1 loads per poll round after
 // `delay` s_sleep periods; false after the spin limit.
 template <int M>
-__device__ __forceinline__ bool ld_granules(const uint64_t* src, uint32_t (&w)[M], unsigned tag, int delay,
+__device__ __forceinline__ bool ld_granules(const uint64_t* src, int stride, uint32_t (&w)[M], unsigned tag, int delay,
                                             unsigned spin_limit) {
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
     uint64_t v[M];
@@ -149,7 +153,8 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* src, uint32_t (&w)[M
         bool miss = false;
 #pragma unroll
         for (int t = 0; t < M; t++) {
-            v[t] = src ? __hip_atomic_load(src + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (uint64_t)tag << 32;
+            v[t] = src ? __hip_atomic_load(src + (int64_t)t * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : (uint64_t)tag << 32;
             miss = miss || (unsigned)(v[t] >> 32) != tag;
         }
         if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
@@ -219,8 +224,9 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
 
     const int up = band > 0 ? band - 1 : (BOUNDED ? -1 : a.nb - 1);
     const int dn = band + 1 < a.nb ? band + 1 : (BOUNDED ? -1 : 0);
+    // granule of word 0 of (parity, band b, side, row e) for this lane's window and half; word t is 2K further
     auto xrow = [&](int parity, int b, int side, int e) {
-        return a.xch + ((((((int64_t)parity * a.nb + b) * 2 + side) * K + e) * nx + x) * 2 + h) * M;
+        return a.xch + (((((int64_t)parity * a.nb + b) * 2 + side) * nx + x) * M) * (2 * K) + h * K + e;
     };
     auto tag_of = [&](int blk) { return a.epoch << 16 | (unsigned)(blk + 1); };
 
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
                                                                           __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
                 failed = true;
             if (!failed && __builtin_amdgcn_ballot_w64(src != nullptr) != 0 &&
-                !ld_granules<M>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit)) {
+                !ld_granules<M>(src, 2 * K, w, tag_of(blk - 1), a.poll_delay, a.spin_limit)) {
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 failed = true;
             }
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
 #pragma unroll
             for (int side = 0; side < 2; side++) {
                 const int e = side == 0 ? r - K : r - B;
-                if (e >= 0 && e < K && r < L) st_granules<M>(xrow(par, band, side, e), w, tag_of(blk));
+                if (e >= 0 && e < K && r < L) st_granules<M>(xrow(par, band, side, e), 2 * K, w, tag_of(blk));
             }
         }
     }
@@ -433,6 +439,7 @@ hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int6
         }
     }
     void* args[] = {&a};
+    if (tune.plain_launch) return hipLaunchKernel(fn, dim3(p.nb), dim3(64 * p.nx), args, lds, s);
     return hipLaunchCooperativeKernel(fn, dim3(p.nb), dim3(64 * p.nx), args, (unsigned)lds, s);
 }
 

@@ -125,8 +125,8 @@ def lane_pass(board, gens, K, bounded, m_opt=0):
 
     xch = {}
 
-    def xrow(parity, b, side, e, x, hh):
-        return (((((parity * nb + b) * 2 + side) * K + e) * nx + x) * 2 + hh) * M
+    def xrow(parity, b, side, e, x, hh):  # word t at + 2K t
+        return ((((parity * nb + b) * 2 + side) * nx + x) * M) * (2 * K) + hh * K + e
 
     nblk = -(-gens // K)
     for blk in range(nblk):
@@ -144,7 +144,7 @@ def lane_pass(board, gens, K, bounded, m_opt=0):
                         elif K + bd["B"] <= r[l] < bd["L"] and dn >= 0:
                             src = xrow(par, dn, 0, r[l] - K - bd["B"], x, h[l])
                         if src is not None:
-                            win["w"][l] = [xch[(src + t, blk - 1)] for t in range(M)]
+                            win["w"][l] = [xch[(src + 2 * K * t, blk - 1)] for t in range(M)]
         for bd in bands:
             for win in bd["wins"]:
                 w = win["w"]
@@ -196,7 +196,8 @@ def lane_pass(board, gens, K, bounded, m_opt=0):
                         if 0 <= e < K and r[l] < bd["L"]:
                             base = xrow(par, band, side, e, x, h[l])
                             for t in range(M):
-                                xch[(base + t, blk)] = win["w"][l, t]
+                                assert (base + 2 * K * t, blk) not in xch  # every granule written once per block
+                                xch[(base + 2 * K * t, blk)] = win["w"][l, t]
     out = np.zeros((H, nw), np.uint32)
     for bd in bands:
         for x, win in enumerate(bd["wins"]):
