@@ -232,8 +232,9 @@ struct BoardOptions {
     bool lanes = false;                       // "lanes": rows-on-lanes band pass (gol_lanes.hip) where it applies,
                                               // in place of the cooperative pass, for calls of >= 2 * coop depth
     int lanes_m = 0;                          // "lanes_m": its words per lane and half-row (0 = by width, 5, 9, 17)
-    bool coop_launch = true;                  // "coop_launch": persistent passes by hipLaunchCooperativeKernel (0:
-                                              // hipLaunchKernel; their grids fit the device by construction)
+    bool coop_launch = false;                 // "coop_launch": persistent passes by hipLaunchCooperativeKernel (1), or
+                                              // hipLaunchKernel after the same residency check (0, the default:
+                                              // gol_internal.h launch_persistent)
 };
 
 struct gol_board {

@@ -23,9 +23,10 @@
 // a band rewrites parity p after both neighbours have published the next block, which they do after reading
 // parity p; the epoch keeps a granule of an earlier launch from matching (the host clears the buffer when the
 // 16-bit epoch wraps).  The board buffers are only read at the start and written at the end (kernel boundaries
-// order those).  Residency: the grid is one workgroup per CU (LDS request above half the CU's), launched
-// cooperatively; every spin is bounded, and a timed-out wait raises an error word the host checks on the next
-// synchronisation.
+// order those).  Residency: the grid is one workgroup per CU (LDS request above half the CU's), checked against the
+// occupancy API before a plain launch (launch_persistent below; round 4: the cooperative launch API's exit-time
+// teardown faulted under rocprofv3); every spin is bounded, and a timed-out wait raises an error word the host
+// checks on the next synchronisation.
 #include "gol_internal.h"
 #include "gol_bitlogic.h"
 
@@ -568,8 +569,37 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
         }
     }
     void* args[] = {&a};
-    if (tune.plain_launch) return hipLaunchKernel(fn, dim3(nwg), dim3(kThreads), args, lds, s);
-    return hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(kThreads), args, (unsigned)lds, s);
+    return launch_persistent(fn, (unsigned)nwg, kThreads, args, lds, s, !tune.plain_launch);
+}
+
+hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, void** args, size_t lds, hipStream_t s,
+                             bool cooperative) {
+    if (cooperative) return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
+    struct Fit {
+        const void* fn;
+        unsigned threads;
+        size_t lds;
+        int64_t resident;  // workgroups the device holds at once
+    };
+    static std::mutex mu;
+    static std::vector<Fit> fits;
+    int64_t resident = -1;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        for (const Fit& f : fits)
+            if (f.fn == fn && f.threads == threads && f.lds == lds) resident = f.resident;
+        if (resident < 0) {
+            int per_cu = 0, dev = 0, cus = 0;
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)threads, lds);
+            if (e == hipSuccess) e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e != hipSuccess) return e;
+            resident = (int64_t)per_cu * cus;
+            fits.push_back({fn, threads, lds, resident});
+        }
+    }
+    if ((int64_t)grid > resident) return hipErrorCooperativeLaunchTooLarge;
+    return hipLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, s);
 }
 
 }  // namespace gol

@@ -123,6 +123,14 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
                             int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
                             hipStream_t s, int64_t ragged_w = 0, const CoopTuning& tune = CoopTuning());
 
+// A persistent launch whose workgroups wait on each other (the cooperative and rows-on-lanes passes): every
+// workgroup must be resident at once.  cooperative: hipLaunchCooperativeKernel; else hipLaunchKernel after the same
+// check against the occupancy API (hipErrorCooperativeLaunchTooLarge when the grid cannot be resident).  The plain
+// launch is the default (board option "coop_launch"): the runtime's cooperative-launch state is torn down at process
+// exit after a profiler's (rocprofv3 --kernel-trace) and faulted there (DESIGN.md 6 "Exit under rocprofv3").
+hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, void** args, size_t lds, hipStream_t s,
+                             bool cooperative);
+
 // ---- gol_lanes.hip: rows-on-lanes band pass (a wave owns all rows of a band window of 64 (m - 1) columns and
 // steps it k generations alone), packed boards of any interleave, W a multiple of 64 (m - 1), k <= 16
 struct LanesPlan {

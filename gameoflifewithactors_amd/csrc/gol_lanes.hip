@@ -439,8 +439,7 @@ hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int6
         }
     }
     void* args[] = {&a};
-    if (tune.plain_launch) return hipLaunchKernel(fn, dim3(p.nb), dim3(64 * p.nx), args, lds, s);
-    return hipLaunchCooperativeKernel(fn, dim3(p.nb), dim3(64 * p.nx), args, (unsigned)lds, s);
+    return launch_persistent(fn, (unsigned)p.nb, (unsigned)(64 * p.nx), args, lds, s, !tune.plain_launch);
 }
 
 }  // namespace gol
