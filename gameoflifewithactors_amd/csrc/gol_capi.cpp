@@ -229,8 +229,9 @@ struct BoardOptions {
     int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
     int resident_threads = 1024;              // "resident_threads": LDS-resident workgroup size (1024 or 256)
-    bool lanes = false;                       // "lanes": rows-on-lanes band pass (gol_lanes.hip) where it applies,
-                                              // in place of the cooperative pass, for calls of >= 2 * coop depth
+    int lanes = 2;                            // "lanes": rows-on-lanes band pass (gol_lanes.hip) in place of the
+                                              // cooperative one, for calls of >= 2 * coop depth: 2 = where it
+                                              // measured faster (use_lanes), 1 = wherever it applies, 0 = never
     int lanes_m = 0;                          // "lanes_m": its words per lane and half-row (0 = by width, 5, 9, 17)
     bool coop_launch = false;                 // "coop_launch": persistent passes by hipLaunchCooperativeKernel (1), or
                                               // hipLaunchKernel after the same residency check (0, the default:
@@ -463,8 +464,15 @@ int coop_depth(const gol_board* b) {
 // The rows-on-lanes band pass (gol_lanes.hip) on a packed single board, for a call of `gens` generations: the boards
 // the cooperative pass would take whose width splits into windows (64 (m - 1) columns each), calls of at least two
 // hand-off blocks (the pass stages the board through LDS at both ends of a launch).
+// By default (option "lanes" 2) it takes the sizes where it measured faster than the cooperative pass
+// (profiles/r4/lanes_ab_j.log, us/generation, lanes vs cooperative): rows of <= 1024 cells (m = 5: 256^2 0.35 vs
+// 0.49, 512^2 0.37 vs 0.49, 1024 x 2048 0.41 vs 0.51) and 8192-wide boards up to 4096 rows (m = 9: 8192 x 2048 1.08
+// vs 1.55, 8192 x 4096 1.20 vs 1.63); the cooperative pass keeps 2048- and 4096-wide boards (4096^2 0.74 vs 0.69,
+// 2048 x 1024 0.50 vs 0.43) and taller 8192-wide ones (8192^2 3.1 vs 1.9).
+bool lanes_by_size(int64_t W, int64_t H) { return W <= 1024 || (W == 8192 && H <= 4096); }
 bool use_lanes(const gol_board* b, int64_t gens) {
     if (!b->opt.lanes || !b->opt.coop || !b->packed || b->multi) return false;
+    if (b->opt.lanes == 2 && !lanes_by_size(b->W, b->H)) return false;
     gol::LanesPlan p;
     return gens >= 2 * coop_depth(b) && b->W * b->H <= b->opt.coop_max_cells &&
            gol::lanes_plan(b->W, b->H, coop_depth(b), b->opt.lanes_m, &p);
@@ -1420,7 +1428,10 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (value < 0 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be 0..4096");
         o.coop_poll_delay = (int)value;
     } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
-    else if (n == "lanes") o.lanes = value != 0;
+    else if (n == "lanes") {
+        if (value < 0 || value > 2) return fail(GOL_ERR_INVALID, "lanes must be 0, 1 or 2 (by size)");
+        o.lanes = (int)value;
+    }
     else if (n == "coop_launch") o.coop_launch = value != 0;
     else if (n == "lanes_m") {
         if (value != 0 && value != 5 && value != 9 && value != 17) return fail(GOL_ERR_INVALID, "lanes_m must be 0, 5, 9 or 17");

@@ -39,6 +39,11 @@ namespace {
 constexpr int kWinRows = 32;                // window rows: one per lane of a half
 constexpr int kXchCells = 16;               // halo cells refreshed between blocks (K <= kXchCells)
 constexpr unsigned kLaneSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident
+// Cost decomposition builds (A/B only, wrong results): 1 = no hand-off (no granule stores or polls), 2 = no hand-off
+// and no edge swap between the windows (the generation loops alone)
+#ifndef GOL_LANES_DECOMP
+#define GOL_LANES_DECOMP 0
+#endif
 
 struct LaneArgs {
     const uint32_t* src;  // board at launch
@@ -234,7 +239,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
     bool failed = false;
     for (int blk = 0; blk < nblk; blk++) {
         const int k = a.gens - blk * K < K ? a.gens - blk * K : K;
-        if (blk > 0) {
+        if (GOL_LANES_DECOMP == 0 && blk > 0) {
             // the halo rows: the same window of the neighbour bands' edge rows, block blk - 1
             const int par = (blk - 1) & 1;
             const uint64_t* src = nullptr;
@@ -275,7 +280,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
         }
         if (blk + 1 == nblk) break;
         // ---- the cells beside the useful edges, between the band's windows (LDS, one barrier)
-        {
+        if (GOL_LANES_DECOMP < 2) {
             const int par = blk & 1;
             uint32_t e = 0;  // cells [32, 48) of the half: the useful edge (h = 0: left, h = 1: right, reversed)
 #pragma unroll
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
             }
         }
         // ---- hand-off: the band's first and last K rows (a band shorter than 2K rows sends some to both sides)
-        {
+        if (GOL_LANES_DECOMP == 0) {
             const int par = blk & 1;
 #pragma unroll
             for (int side = 0; side < 2; side++) {
@@ -365,7 +370,8 @@ bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out) {
         for (int c : kLaneM)
             if (c == m_opt) m = c;
     } else {
-        m = W % 512 == 0 ? 9 : (W % 256 == 0 ? 5 : 0);
+        // narrow rows: 256-column windows (more waves on a small board); wide rows: 512 (fewer halo columns)
+        m = W <= 1024 ? (W % 256 == 0 ? 5 : 0) : (W % 512 == 0 ? 9 : (W % 256 == 0 ? 5 : 0));
     }
     if (!m) return false;
     const int64_t u = 64 * (m - 1);

@@ -22,7 +22,12 @@ def lanes_plan(W, H, k, m_opt=0):
     """gol_lanes.hip lanes_plan."""
     if W < 256 or W % 32 or W > 16384 or H < 3 or k < 1 or k > XCH_CELLS:
         return None
-    m = m_opt if m_opt in (5, 9, 17) else (0 if m_opt else (9 if W % 512 == 0 else (5 if W % 256 == 0 else 0)))
+    if m_opt:
+        m = m_opt if m_opt in (5, 9, 17) else 0
+    elif W <= 1024:
+        m = 5 if W % 256 == 0 else 0
+    else:
+        m = 9 if W % 512 == 0 else (5 if W % 256 == 0 else 0)
     if not m:
         return None
     u = 64 * (m - 1)
