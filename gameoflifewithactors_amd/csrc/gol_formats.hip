@@ -323,6 +323,20 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
+// One atomic per workgroup (256 threads): every atomicAdd on the single accumulator is a serialized device-scope
+// round trip (the per-XCD L2s are not coherent), so one per wave made a 4096^2 population take ~100 us
+// (profiles/r4/trace_c2_kernel_stats_j.csv) for 2 MiB of reads.
+__device__ __forceinline__ void block_add(uint64_t sum, unsigned long long* acc) {
+    __shared__ uint64_t part[4];
+    sum = wave_sum_u64(sum);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t t = part[0] + part[1] + part[2] + part[3];
+        if (t) atomicAdd(acc, (unsigned long long)t);
+    }
+}
+
 // population (any packed layout): adds the popcount of rows [row0, row0+rows) into *acc
 __global__ void gol_popcount_packed(const uint32_t* __restrict__ words, int64_t wpr, int64_t rows, int64_t pitch,
                                     int64_t row0, unsigned long long* acc) {
@@ -330,16 +344,14 @@ __global__ void gol_popcount_packed(const uint32_t* __restrict__ words, int64_t 
     const int64_t n = wpr * rows;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x)
         sum += __popc(words[(row0 + idx / wpr) * pitch + idx % wpr]);
-    sum = wave_sum_u64(sum);
-    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(acc, (unsigned long long)sum);
+    block_add(sum, acc);
 }
 
 __global__ void gol_popcount_bytes(const uint8_t* __restrict__ cells, int64_t n, unsigned long long* acc) {
     uint64_t sum = 0;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (int64_t)gridDim.x * blockDim.x)
         sum += cells[idx] != 0;
-    sum = wave_sum_u64(sum);
-    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(acc, (unsigned long long)sum);
+    block_add(sum, acc);
 }
 
 // Canonical 64-cell chunk j of a packed row r (layout ilv): bit i = cell 64j + i, zero past the width.
@@ -373,8 +385,7 @@ __global__ void gol_hash_packed(const uint32_t* __restrict__ words, int64_t W, i
         const uint64_t key = (uint64_t)((gy0 + y) * nc + j);
         sum += fmix64(v ^ fmix64(key + 0x9E3779B97F4A7C15ULL));
     }
-    sum = wave_sum_u64(sum);
-    if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)sum);
+    block_add(sum, acc);
 }
 
 __global__ void gol_hash_bytes(const uint8_t* __restrict__ cells, int64_t W, int64_t H, unsigned long long* acc) {
@@ -387,8 +398,7 @@ __global__ void gol_hash_bytes(const uint8_t* __restrict__ cells, int64_t W, int
         for (int b = 0; b < 64 && j * 64 + b < W; b++) v |= (uint64_t)(cells[y * W + j * 64 + b] != 0) << b;
         sum += fmix64(v ^ fmix64((uint64_t)idx + 0x9E3779B97F4A7C15ULL));
     }
-    sum = wave_sum_u64(sum);
-    if ((threadIdx.x & 63) == 0) atomicAdd(acc, (unsigned long long)sum);
+    block_add(sum, acc);
 }
 
 // set the cells listed as (x, y) pairs (RLE placement); ilv == 0: byte board
@@ -454,9 +464,10 @@ static inline unsigned grid1d(int64_t n, int block = 256) {
     int64_t g = (n + block - 1) / block;
     return (unsigned)(g < 1 ? 1 : g);
 }
-static inline unsigned grid_stride(int64_t n, int block = 256) {
-    int64_t g = (n + block - 1) / block;
-    if (g > 8192) g = 8192;
+// reductions (one atomic per workgroup): at least 16 elements per thread, at most 1024 workgroups
+static inline unsigned grid_reduce(int64_t n, int block = 256) {
+    int64_t g = n / ((int64_t)block * 16);
+    if (g > 1024) g = 1024;
     return (unsigned)(g < 1 ? 1 : g);
 }
 
@@ -556,25 +567,25 @@ hipError_t launch_splitmix_bytes(uint8_t* cells, int64_t W, int64_t H, uint64_t 
 
 hipError_t launch_popcount_packed(const uint32_t* words, int64_t wpr, int64_t rows, int64_t pitch, int64_t row0,
                                   unsigned long long* acc, hipStream_t s) {
-    hipLaunchKernelGGL(gol_popcount_packed, dim3(grid_stride(wpr * rows)), dim3(256), 0, s, words, wpr, rows, pitch,
+    hipLaunchKernelGGL(gol_popcount_packed, dim3(grid_reduce(wpr * rows)), dim3(256), 0, s, words, wpr, rows, pitch,
                        row0, acc);
     return hipGetLastError();
 }
 
 hipError_t launch_popcount_bytes(const uint8_t* cells, int64_t n, unsigned long long* acc, hipStream_t s) {
-    hipLaunchKernelGGL(gol_popcount_bytes, dim3(grid_stride(n)), dim3(256), 0, s, cells, n, acc);
+    hipLaunchKernelGGL(gol_popcount_bytes, dim3(grid_reduce(n)), dim3(256), 0, s, cells, n, acc);
     return hipGetLastError();
 }
 
 hipError_t launch_hash_packed(const uint32_t* words, int64_t W, int64_t rows, int64_t pitch, int64_t row0,
                               int64_t gy0, int ilv, unsigned long long* acc, hipStream_t s) {
-    hipLaunchKernelGGL(gol_hash_packed, dim3(grid_stride((W + 63) / 64 * rows)), dim3(256), 0, s, words, W, rows, pitch,
+    hipLaunchKernelGGL(gol_hash_packed, dim3(grid_reduce((W + 63) / 64 * rows)), dim3(256), 0, s, words, W, rows, pitch,
                        row0, gy0, ilv, acc);
     return hipGetLastError();
 }
 
 hipError_t launch_hash_bytes(const uint8_t* cells, int64_t W, int64_t H, unsigned long long* acc, hipStream_t s) {
-    hipLaunchKernelGGL(gol_hash_bytes, dim3(grid_stride((W + 63) / 64 * H)), dim3(256), 0, s, cells, W, H, acc);
+    hipLaunchKernelGGL(gol_hash_bytes, dim3(grid_reduce((W + 63) / 64 * H)), dim3(256), 0, s, cells, W, H, acc);
     return hipGetLastError();
 }
 
