@@ -10,22 +10,12 @@ step() {  # step NAME SECONDS CMD...
   if [ $rc -ge 124 ]; then tail -20 $O/$name.log; echo "stopping after $name (rc $rc)"; exit $rc; fi
   return 0
 }
-step lanes_ab 300 python tools/lanes_ab.py --rounds 3
-grep '^{' $O/lanes_ab.log | cut -c1-150
-step bench_n1_a 300 python bench.py --gpus 1 --steps 20 --warmup 5
+step bench_n1_a 400 python bench.py --gpus 1 --steps 20 --warmup 5
 grep -o '"value": [0-9.]*\|"verify": {[^}]*}\|"avg_launch_us": [0-9.]*\|"value_device_events": [0-9.]*\|"first_generation_timed": [0-9]*' $O/bench_n1_a.log | tr '\n' ' '; echo
-for split in 0.66 0.70 0.74 0.62 0.68 0.72; do
-  step split_$split 120 python tools/sweep.py --ilv 2 --ks 12 --passes 16 --pre 300 --split $split
-  grep '^{' $O/split_$split.log | cut -c1-120
-done
 step bench_bounded 300 python bench.py --gpus 1 --steps 20 --warmup 5 --boundary bounded --no-cpu-baseline
 grep -o '"value": [0-9.]*\|"verify": {[^}]*}\|"avg_launch_us": [0-9.]*' $O/bench_bounded.log | tr '\n' ' '; echo
-step pmc_torus 600 bash tools/pmc_traffic.sh torus 12
-tail -2 $O/pmc_torus.log
-step pmc_bounded 600 bash tools/pmc_traffic.sh bounded 12
-tail -2 $O/pmc_bounded.log
-step pmc_sq_torus 300 bash tools/pmc.sh r4_torus_k12 12 2 "3 4"
-PMC_BOUNDARY=1 step pmc_sq_bounded 300 bash tools/pmc.sh r4_bounded_k12 12 2 "3 4"
+step bench_c5 120 python bench.py --init rle:gosper-gun@10,10+r-pentomino@180,150 --width 256 --height 256 --boundary bounded --generations 100000 --gens-per-step 50000 --steps 1 --warmup 1
+grep -o '"us_per_generation[a-z_]*": [0-9.]*\|"ok": [a-z]*' $O/bench_c5.log | tr '\n' ' '; echo
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/trace_bench -o run -- python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-verify --handle-parts 0 > $GRAFT_REPO_ROOT/$O/trace_bench.log 2>&1; echo "== trace_bench rc=$?"
 grep -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' $GRAFT_REPO_ROOT/$O/trace_bench.log | tr '\n' ' '; echo
