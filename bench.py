@@ -106,6 +106,7 @@ def parse():
                    "verify generation; -1 = the world size (1: the single board); 0 = off")
     p.add_argument("--verify-gen", type=int, default=-1, help=argparse.SUPPRESS)
     p.add_argument("--handle-first-gen", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--handle-transport", choices=["default", "rccl"], default="default", help=argparse.SUPPRESS)
     p.add_argument("--no-verify", action="store_true",
                    help="skip the untimed self-check (step to the next golden checkpoint and compare hashes)")
     return p.parse_args()
@@ -243,10 +244,10 @@ def handle_leg(args, W, H, boundary, parts, ndev):
     from gameoflifewithactors_amd import _lib
 
     devices = [i % ndev for i in range(parts)]
-    out = {"strips": parts, "devices": devices, "hip_runtime": None}
-    runs = {"single" if parts == 1 else "peer": None}
-    if parts > 1 and len(set(devices)) == parts:
-        runs["rccl"] = None
+    out = {"strips": parts, "devices": devices, "hip_runtime": None,
+           "rccl_possible": parts > 1 and len(set(devices)) == parts}
+    # one transport per child process (run_handle_leg): an RCCL run that fails or hangs costs only itself
+    runs = {"rccl": None} if args.handle_transport == "rccl" else {"single" if parts == 1 else "peer": None}
     for name in runs:
         try:
             runs[name] = _handle_run(args, W, H, boundary, devices, name)
@@ -259,25 +260,36 @@ def handle_leg(args, W, H, boundary, parts, ndev):
     return out
 
 
-def run_handle_leg(args, W, H, boundary, parts, verify_gen, first_gen=0):
-    """The handle leg in a child process of rank 0 under a time limit: it may create an RCCL communicator over all
-    GPUs inside one process, and a failure or hang there must not cost the main line.  The child never imports
-    torch (bench.py main)."""
+def _handle_child(args, W, H, parts, verify_gen, first_gen, transport, timeout):
     cmd = [sys.executable, os.path.abspath(__file__), "--handle-leg-child", "--width", str(W), "--height", str(H),
            "--boundary", args.boundary, "--handle-parts", str(parts), "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--seed", str(args.seed), "--verify-gen", str(verify_gen),
-           "--handle-first-gen", str(first_gen)]
+           "--handle-first-gen", str(first_gen), "--handle-transport", transport]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
     env["WORLD_SIZE"] = "1"
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.handle_timeout, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     except subprocess.TimeoutExpired:
-        return {"error": f"handle leg exceeded {args.handle_timeout:.0f} s (killed)"}
+        return {"error": f"handle leg ({transport}) exceeded {timeout:.0f} s (killed)"}
     if r.returncode != 0:
-        return {"error": f"handle leg exited {r.returncode}: {r.stderr.strip()[-600:]}"}
+        return {"error": f"handle leg ({transport}) exited {r.returncode}: {r.stderr.strip()[-600:]}"}
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def run_handle_leg(args, W, H, boundary, parts, verify_gen, first_gen=0):
+    """The handle leg in child processes of rank 0, each under a time limit and never importing torch (bench.py
+    main): the default transport first, then -- when every strip has its own GPU -- RCCL in a second child, since
+    it creates a communicator over all GPUs inside one process and a failure or hang there must cost neither the
+    main line nor the peer-copy figures."""
+    del boundary
+    out = _handle_child(args, W, H, parts, verify_gen, first_gen, "default", args.handle_timeout)
+    if "error" in out or not out.get("rccl_possible"):
+        return out
+    rccl = _handle_child(args, W, H, parts, verify_gen, first_gen, "rccl", min(args.handle_timeout, 180.0))
+    out.setdefault("runs", {})["rccl"] = rccl.get("runs", {}).get("rccl", rccl) if "error" not in rccl else rccl
+    return out
 
 
 def traffic_key(W, rows, boundary, k, ilv):
@@ -413,7 +425,7 @@ def main():
             # host-side barrier for the handle leg: the waiting ranks must not keep an RCCL kernel spinning
             # on the devices rank 0's one-process board is running on
             host_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=max(
-                120, args.handle_timeout + 60)))
+                120, args.handle_timeout + min(args.handle_timeout, 180.0) + 60)))
         else:
             dist.init_process_group("gloo", timeout=timeout)
             host_group = dist.group.WORLD

@@ -470,12 +470,20 @@ int coop_depth(const gol_board* b) {
 // vs 1.55, 8192 x 4096 1.20 vs 1.63); the cooperative pass keeps 2048- and 4096-wide boards (4096^2 0.74 vs 0.69,
 // 2048 x 1024 0.50 vs 0.43) and taller 8192-wide ones (8192^2 3.1 vs 1.9).
 bool lanes_by_size(int64_t W, int64_t H) { return W <= 1024 || (W == 8192 && H <= 4096); }
+// Its hand-off depth: the "coop_k" option if set, else up to 10 on rows of <= 1024 cells (the deepest a 32-row
+// window holds beside a band of >= k rows; there the pass is hand-off bound: 256^2 bounded 0.32 vs 0.36 us/generation
+// at k = 8, 512^2 0.33 vs 0.37, 1024 x 2048 0.36 vs 0.41, profiles/r4/lanes_k_o.log), else the cooperative depth.
+int lanes_depth(const gol_board* b) {
+    if (b->opt.coop_k > 0) return b->opt.coop_k;
+    if (b->W > 1024) return coop_depth(b);
+    return b->tblock_set && b->tblock < 10 ? b->tblock : 10;
+}
 bool use_lanes(const gol_board* b, int64_t gens) {
     if (!b->opt.lanes || !b->opt.coop || !b->packed || b->multi) return false;
     if (b->opt.lanes == 2 && !lanes_by_size(b->W, b->H)) return false;
     gol::LanesPlan p;
-    return gens >= 2 * coop_depth(b) && b->W * b->H <= b->opt.coop_max_cells &&
-           gol::lanes_plan(b->W, b->H, coop_depth(b), b->opt.lanes_m, &p);
+    return gens >= 2 * lanes_depth(b) && b->W * b->H <= b->opt.coop_max_cells &&
+           gol::lanes_plan(b->W, b->H, lanes_depth(b), b->opt.lanes_m, &p);
 }
 
 bool use_coop(const gol_board* b) {
@@ -517,7 +525,7 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
         GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
     }
     int nwg = 0, B = 0, R = 0;
-    const int k = coop_depth(b);
+    const int k = lanes ? lanes_depth(b) : coop_depth(b);
     int64_t need = 0;
     if (lanes) {
         gol::LanesPlan lp;

@@ -78,11 +78,13 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 // Prefetch placement of the deep passes on seam strips (torus), GOL_SEAM_SPREAD: 0 = all R rows' DMAs at the trip's
 // top (the bounded passes' placement), 1 = one row's DMAs after each of the first R generation levels, 3 = the rows'
 // own-word DMAs at the top and one row's seam DMAs after each of the first R levels, 4 = row r's own-word DMAs after
-// level 2r and its seam DMAs after level 2r + 1; -1 (default) = 4 at K >= 16, else 1.  Rows a short pass (K below the
+// level 2r and its seam DMAs after level 2r + 1; -1 (default) = 4.  Rows a short pass (K below the
 // levels a mode needs) has not issued by its last level are issued after it; the pipeline-fill trips (which skip
 // levels) keep every DMA at the top.  Round 3, interleaved on one box at generation 300 (profiles/r3/ab_spread_modes_i.log),
 // GCUPS for modes 1 / 0 / 3 / 4: (12, 2) 114.3 / 113.4 / 113.6 / 113.8, (16, 2) 115.2 / 113.0 / 115.4 / 116.5.
 // On bounded boards (no seam DMAs) spreading lost 5 % (profiles/r3/ab_spread_h.log): they keep mode 0.
+// Round 4, one seam DMA per trip (GOL_SEAM1), (12, 2) at generation 300, 3 interleaved rounds (profiles/r4/
+// ab_spread_o.log), us per pass for modes 1 / 0 / 3 / 4: 440.8 / 508.1 / 503.7 / 435.9 -- (12, 2) moves to mode 4.
 #ifndef GOL_SEAM_SPREAD
 #define GOL_SEAM_SPREAD -1
 #endif
@@ -903,7 +905,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             __builtin_amdgcn_sched_barrier(0);  // the row reads before the prefetch: their latency hides behind it
             // prefetch placement (GOL_SEAM_SPREAD above): rows issued at the top, after level g, and after the levels
             // (the pipeline-fill trips, which skip levels, keep every DMA at the top)
-            constexpr int kSpread = GOL_SEAM_SPREAD >= 0 ? GOL_SEAM_SPREAD : (K >= 16 ? 4 : 1);
+            constexpr int kSpread = GOL_SEAM_SPREAD >= 0 ? GOL_SEAM_SPREAD : 4;
             constexpr int kMode = W::kSeam && !decltype(skip)::value ? kSpread : 0;
             if constexpr (kMode == 0) w.template stage_load<1 - PAR>();
             if constexpr (kMode == 3) {

@@ -115,14 +115,14 @@ def test_lanes_epoch_wrap(gol, oracle):
     b0 = _rand(1024, 1024, 78)
     with gol.Board(1024, 1024, 0, options={"lanes": 1}) as b:
         b.set_cells(b0)
-        b.step(17)
-        done = 17
+        b.step(23)  # >= 2 blocks of this width's depth (10)
+        done = 23
         for epoch in (0xfffd, 0xfffe, 0xffff):
             b.set_option("coop_epoch", epoch)
-            b.step(17)
-            done += 17
-        b.step(17)
-        done += 17
+            b.step(23)
+            done += 23
+        b.step(23)
+        done += 23
         assert b.get_option("lanes_launches") == 5
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, done, 0))
 
