@@ -6,7 +6,7 @@ variant, round), with the board's hash so the variants can be seen to agree.
     python tools/lanes_ab.py [--rounds N] [--boards WxHxB,...] [--gens G] [--variants coop,l9,l5,l17,l9k6,...]
 
 A board WxHxB: B = 0 torus, 1 bounded.  Variant names: "coop" (k = default), "coopkN", "coopc" (launched by
-hipLaunchCooperativeKernel: board option coop_launch 1); "lM" (lanes, m = M) and "lMkN" (depth N), "lMdD" (poll
+hipLaunchCooperativeKernel: board option coop_launch 1), "coopdD" (poll delay D); "lM" (lanes, m = M) and "lMkN" (depth N), "lMdD" (poll
 delay D).
 """
 import argparse
@@ -22,11 +22,13 @@ VARIANTS = "coop,l9,l5,l17,l9k6,l9k10,l5k10"
 
 
 def options(name):
-    m = re.fullmatch(r"coop(c?)(?:k(\d+))?", name)
+    m = re.fullmatch(r"coop(c?)(?:k(\d+))?(?:d(\d+))?", name)
     if m:
         o = {"lanes": 0, "coop_launch": 1 if m.group(1) else 0}
         if m.group(2):
             o["coop_k"] = int(m.group(2))
+        if m.group(3):
+            o["coop_poll_delay"] = int(m.group(3))
         return o
     m = re.fullmatch(r"l(\d+)(?:k(\d+))?(?:d(\d+))?", name)
     if not m:
