@@ -78,7 +78,7 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 // Prefetch placement of the deep passes on seam strips (torus), GOL_SEAM_SPREAD: 0 = all R rows' DMAs at the trip's
 // top (the bounded passes' placement), 1 = one row's DMAs after each of the first R generation levels, 3 = the rows'
 // own-word DMAs at the top and one row's seam DMAs after each of the first R levels, 4 = row r's own-word DMAs after
-// level 2r and its seam DMAs after level 2r + 1; -1 (default) = 4.  Rows a short pass (K below the
+// level 2r and its seam DMAs after level 2r + 1, 5 = the same every 3 levels (3r, 3r + 1); -1 (default) = 4.  Rows a short pass (K below the
 // levels a mode needs) has not issued by its last level are issued after it; the pipeline-fill trips (which skip
 // levels) keep every DMA at the top.  Round 3, interleaved on one box at generation 300 (profiles/r3/ab_spread_modes_i.log),
 // GCUPS for modes 1 / 0 / 3 / 4: (12, 2) 114.3 / 113.4 / 113.6 / 113.8, (16, 2) 115.2 / 113.0 / 115.4 / 116.5.
@@ -930,6 +930,14 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
                             w.template stage_load_row<1 - PAR, 2>(g / 2);
                         __builtin_amdgcn_sched_barrier(0);
                     }
+                } else if constexpr (kMode == 5) {  // A/B: row r's DMAs after levels 3r and 3r + 1
+                    if (g < 3 * R && g % 3 < 2) {
+                        if (g % 3 == 0)
+                            w.template stage_load_row<1 - PAR, 1>(g / 3);
+                        else
+                            w.template stage_load_row<1 - PAR, 2>(g / 3);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
             };
             w.template process<decltype(skip)::value, decltype(mask)::value>(B, NV, tt, hook);
@@ -944,6 +952,14 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
                         w.template stage_load_row<1 - PAR, 1>(g / 2);
                     else
                         w.template stage_load_row<1 - PAR, 2>(g / 2);
+                }
+            } else if constexpr (kMode == 5) {
+#pragma unroll
+                for (int g = K; g < 3 * R; g++) {
+                    if (g % 3 == 0)
+                        w.template stage_load_row<1 - PAR, 1>(g / 3);
+                    else if (g % 3 == 1)
+                        w.template stage_load_row<1 - PAR, 2>(g / 3);
                 }
             }
         };

@@ -1,5 +1,5 @@
-# GPU call script (gpurun): cooperative-pass depth and poll delay at config 2's size (plain launch).
+# GPU call script (gpurun): seam DMA placement mode 5 (every 3 levels) against the shipped mode 4, interleaved.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4p; mkdir -p $O
-timeout -k 10 400 python tools/lanes_ab.py --rounds 3 --boards 4096x4096x0,4096x4096x1,2048x2048x0 --variants coop,coopk6,coopk10,coopk12,coopd0,coopd4,coopd16,coopd32 > $O/coop_kd.log 2>&1; rc=$?; echo "coop rc=$rc"; [ $rc -eq 0 ] || exit $rc
+O=gpurun_out/r4q; mkdir -p $O
+AB_PRE=300 timeout -k 10 500 bash tools/ab_rep.sh $O/ab_spread5.log 4 "2:12" gameoflifewithactors_amd/libgol_hip.so build/ab/lib_spread5.so; rc=$?; echo "spread rc=$rc"; [ $rc -eq 0 ] || exit $rc
