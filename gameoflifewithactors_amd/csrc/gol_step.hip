@@ -84,7 +84,8 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 // GCUPS for modes 1 / 0 / 3 / 4: (12, 2) 114.3 / 113.4 / 113.6 / 113.8, (16, 2) 115.2 / 113.0 / 115.4 / 116.5.
 // On bounded boards (no seam DMAs) spreading lost 5 % (profiles/r3/ab_spread_h.log): they keep mode 0.
 // Round 4, one seam DMA per trip (GOL_SEAM1), (12, 2) at generation 300, 3 interleaved rounds (profiles/r4/
-// ab_spread_o.log), us per pass for modes 1 / 0 / 3 / 4: 440.8 / 508.1 / 503.7 / 435.9 -- (12, 2) moves to mode 4.
+// ab_spread_o.log), us per pass for modes 1 / 0 / 3 / 4: 440.8 / 508.1 / 503.7 / 435.9 -- (12, 2) moves to mode 4;
+// mode 5 against 4, 4 rounds on another box: 472.5 / 446.7 (ab_spread5_q.log).
 #ifndef GOL_SEAM_SPREAD
 #define GOL_SEAM_SPREAD -1
 #endif
