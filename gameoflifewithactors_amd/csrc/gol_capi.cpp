@@ -1442,7 +1442,8 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
     }
     else if (n == "coop_launch") o.coop_launch = value != 0;
     else if (n == "lanes_m") {
-        if (value != 0 && value != 5 && value != 9 && value != 17) return fail(GOL_ERR_INVALID, "lanes_m must be 0, 5, 9 or 17");
+        if (value != 0 && value != 3 && value != 5 && value != 9 && value != 17)
+            return fail(GOL_ERR_INVALID, "lanes_m must be 0, 3, 5, 9 or 17");
         o.lanes_m = (int)value;
     }
     else if (n == "resident_threads") {

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
     stage_out<MB>(a, lds, y0, B);
 }
 
-constexpr int kLaneM[] = {5, 9, 17};
+constexpr int kLaneM[] = {3, 5, 9, 17};
 
 template <int M, int MB>
 const void* lane_kernel_mb(bool bounded) {
@@ -354,6 +354,7 @@ const void* lane_kernel_m(int ilv, bool bounded) {
 }
 const void* lane_kernel(int m, int ilv, bool bounded) {
     switch (m) {
+        case 3: return lane_kernel_m<3>(ilv, bounded);
         case 5: return lane_kernel_m<5>(ilv, bounded);
         case 9: return lane_kernel_m<9>(ilv, bounded);
         case 17: return lane_kernel_m<17>(ilv, bounded);

@@ -75,6 +75,14 @@ def test_lanes_one_window_per_band(gol, oracle, w, m):
         np.testing.assert_array_equal(_run(gol, b0, boundary, [40], m=m), oracle.c_run(b0, 40, boundary))
 
 
+@pytest.mark.parametrize("w", [256, 384, 1024])
+def test_lanes_narrow_windows(gol, oracle, w):
+    """3 words per lane and half-row: 128-column windows, 2 to 8 per band."""
+    b0 = _rand(300, w, 3 * w)
+    for boundary in (0, 1):
+        np.testing.assert_array_equal(_run(gol, b0, boundary, [33], m=3), oracle.c_run(b0, 33, boundary))
+
+
 @pytest.mark.parametrize("k", [1, 2, 3, 5, 8, 10])
 def test_lanes_block_depths(gol, oracle, k):
     b0 = _rand(1000, 2048, 50 + k)

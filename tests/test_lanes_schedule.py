@@ -23,7 +23,7 @@ def lanes_plan(W, H, k, m_opt=0):
     if W < 256 or W % 32 or W > 16384 or H < 3 or k < 1 or k > XCH_CELLS:
         return None
     if m_opt:
-        m = m_opt if m_opt in (5, 9, 17) else 0
+        m = m_opt if m_opt in (3, 5, 9, 17) else 0
     elif W <= 1024:
         m = 5 if W % 256 == 0 else 0
     else:
@@ -229,7 +229,7 @@ def test_plan_of_config2():
 
 @pytest.mark.parametrize("bounded", [False, True])
 @pytest.mark.parametrize("W,H,K,m,gens", [(512, 40, 8, 0, 19), (1024, 48, 4, 0, 13), (768, 30, 3, 0, 11),
-                                          (256, 24, 5, 5, 12), (1024, 36, 8, 17, 17)])
+                                          (256, 24, 5, 5, 12), (1024, 36, 8, 17, 17), (384, 30, 8, 3, 18)])
 def test_lane_pass_restatement_matches_oracle(W, H, K, m, gens, bounded):
     board = (np.random.default_rng(W + H + K + bounded).random((H, W)) < 0.4).astype(np.uint8)
     got = lane_pass(board, gens, K, bounded, m)

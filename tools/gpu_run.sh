@@ -1,5 +1,6 @@
-# GPU call script (gpurun): seam DMA placement mode 5 (every 3 levels) against the shipped mode 4, interleaved.
+# GPU call script (gpurun): 128-column lanes windows (m = 3) against 256 (m = 5) on the narrow boards, and their tests.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4q; mkdir -p $O
-AB_PRE=300 timeout -k 10 500 bash tools/ab_rep.sh $O/ab_spread5.log 4 "2:12" gameoflifewithactors_amd/libgol_hip.so build/ab/lib_spread5.so; rc=$?; echo "spread rc=$rc"; [ $rc -eq 0 ] || exit $rc
+O=gpurun_out/r4r; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_lanes.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?; tail -2 $O/pytest.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/lanes_ab.py --rounds 3 --boards 256x256x1,256x256x0,512x512x0,1024x1024x0,1024x2048x0,512x4096x0 --variants coop,l3,l5 > $O/lanes_m3.log 2>&1; rc=$?; echo "lanes rc=$rc"; [ $rc -eq 0 ] || exit $rc
