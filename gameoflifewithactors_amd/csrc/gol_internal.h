@@ -139,7 +139,7 @@ struct LanesPlan {
     int nb = 0;    // bands (workgroups)
     int bmax = 0;  // rows of the tallest band
 };
-// m_opt: 0 = by width (5 up to 1024 columns, else 9 when W % 512 == 0, else 5), or 5 / 9 / 17
+// m_opt: 0 = by width (3 up to 1024 columns, else 9 when W % 512 == 0, else 5), or 3 / 5 / 9 / 17
 bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out);
 int64_t lanes_xch_words(const LanesPlan& p, int k);
 // as launch_coop_pass (gens <= 65535 per launch, epoch-tagged granules in xch, *err on a timed-out wait)

@@ -371,8 +371,10 @@ bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out) {
         for (int c : kLaneM)
             if (c == m_opt) m = c;
     } else {
-        // narrow rows: 256-column windows (more waves on a small board); wide rows: 512 (fewer halo columns)
-        m = W <= 1024 ? (W % 256 == 0 ? 5 : 0) : (W % 512 == 0 ? 9 : (W % 256 == 0 ? 5 : 0));
+        // narrow rows: 128-column windows (more, shorter waves on a small board: 256^2 bounded 0.28 vs 0.32 us per
+        // generation at 256 columns, 512^2 0.28 vs 0.33, 512 x 4096 0.33 vs 0.39, profiles/r4/lanes_m3_r.log); wide
+        // rows: 512 (fewer halo columns)
+        m = W <= 1024 ? (W % 128 == 0 ? 3 : 0) : (W % 512 == 0 ? 9 : (W % 256 == 0 ? 5 : 0));
     }
     if (!m) return false;
     const int64_t u = 64 * (m - 1);

@@ -187,10 +187,10 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
  *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)
  *   "lanes" 2 | 1 | 0            rows-on-lanes band pass in place of the cooperative one (packed single boards whose
- *                                width splits into 256/512/1024-column windows, coop_k <= 10, calls of >= 2 coop_k
+ *                                width splits into 128/256/512/1024-column windows, coop_k <= 10, calls of >= 2 k
  *                                generations): 2 = on the sizes it measured faster (rows of <= 1024
  *                                cells; 8192 wide up to 4096 rows), 1 = wherever it applies, 0 = never
- *   "lanes_m" 0 | 3 | 5 | 9 | 17 its words per lane and half-row (0: 5 up to 1024 columns, else 9 when W % 512 == 0)
+ *   "lanes_m" 0 | 3 | 5 | 9 | 17 its words per lane and half-row (0: 3 up to 1024 columns, else 9 when W % 512 == 0)
  *   "coop_launch" 0 | 1          the persistent passes by hipLaunchKernel after a residency check (0), or by
  *                                hipLaunchCooperativeKernel (1; DESIGN.md 6 "Exit under rocprofv3")
  *   "lanes_launches" (read-only) launches of that pass on this board (tests)

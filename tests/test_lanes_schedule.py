@@ -25,7 +25,7 @@ def lanes_plan(W, H, k, m_opt=0):
     if m_opt:
         m = m_opt if m_opt in (3, 5, 9, 17) else 0
     elif W <= 1024:
-        m = 5 if W % 256 == 0 else 0
+        m = 3 if W % 128 == 0 else 0
     else:
         m = 9 if W % 512 == 0 else (5 if W % 256 == 0 else 0)
     if not m:
