@@ -5,7 +5,7 @@ side as m interleaved words per lane and half-row, the second half mirrored -- a
 LDS traffic; between blocks the windows of a band swap their edge cells through LDS and the bands hand their k edge
 rows to their neighbours as tagged granules.  Bar: bit-exact against the oracle (GameOfLifeLogic.fs:59-63; torus
 GameOfLifeDriver.fs:21-25; bounded Script.fsx:6-13) and the BASELINE config-2 golden checkpoints.  Covered: every
-window width (m = 5, 9, 17), one window per band (the torus wraps a window onto itself), up to 16 per band, uneven
+window width (m = 3, 5, 9, 17), one window per band (the torus wraps a window onto itself), up to 16 per band, uneven
 bands, bands shorter than 2k, depths 1-10, board interleaves 1 / 2 / 4, calls too short for the pass between calls
 that take it, the epoch wrap and a timed-out hand-off.  Each case checks that the pass actually ran
 ("lanes_launches").
