@@ -226,7 +226,8 @@ struct BoardOptions {
                                               // layouts: 1 from kRingMinCells cells, 2 always, 0 never (ilv-1 rows,
                                               // bit-level row ends on a torus)
     int coop_r = 1;                           // "coop_r": cooperative pass, rows per wave at least
-    int coop_poll_delay = 8;                  // "coop_poll_delay": s_sleep periods before a hand-off's first poll
+    int coop_poll_delay = -1;                 // "coop_poll_delay": s_sleep periods before a hand-off's first poll
+                                              // (-1: 0 on the cooperative pass's rows of <= 2048 cells, else 8)
     int64_t coop_spin_limit = 0;              // "coop_spin_limit": polls before a hand-off wait gives up (0 = ~2 s)
     int resident_threads = 1024;              // "resident_threads": LDS-resident workgroup size (1024 or 256)
     int lanes = 2;                            // "lanes": rows-on-lanes band pass (gol_lanes.hip) in place of the
@@ -548,7 +549,10 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     }
     gol::CoopTuning tune;
     tune.min_rows = b->opt.coop_r;
-    tune.poll_delay = b->opt.coop_poll_delay;
+    // first-poll delay: rows of one word per lane (<= 2048 cells) hand off sooner than a delay of 8 (~250 ns) waits;
+    // 2048^2 0.42 vs 0.44 us/generation, 2048 x 1024 0.40 vs 0.43, but 4096 x 2048 0.69 vs 0.65 and 4096^2 0.69 vs
+    // 0.68 (profiles/r4/coop_d_t.log); the rows-on-lanes pass keeps 8 (level at 4096^2, lanes_ab_h.log)
+    tune.poll_delay = b->opt.coop_poll_delay >= 0 ? b->opt.coop_poll_delay : (!lanes && W <= 2048 ? 0 : 8);
     tune.spin_limit = (unsigned)std::min<int64_t>(b->opt.coop_spin_limit, 0xffffffffLL);
     tune.plain_launch = !b->opt.coop_launch;
     while (gens > 0) {
@@ -1433,7 +1437,7 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
         o.coop_r = (int)value;
     } else if (n == "coop_poll_delay") {
-        if (value < 0 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be 0..4096");
+        if (value < -1 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be -1 (auto) or 0..4096");
         o.coop_poll_delay = (int)value;
     } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
     else if (n == "lanes") {

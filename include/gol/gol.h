@@ -183,7 +183,9 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *                                never (0: ilv-1 rows)
  *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
  *                                words (0: the per-generation byte step)
- *   "coop_r" 1..8, "coop_poll_delay" 8, "resident_threads" 1024 | 256: A/B experiments
+ *   "coop_poll_delay" -1 | 0..4096  s_sleep periods before a hand-off's first poll (-1: 0 on cooperative-pass rows of
+ *                                <= 2048 cells, else 8)
+ *   "coop_r" 1..8, "resident_threads" 1024 | 256: A/B experiments
  *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
  *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)
  *   "lanes" 2 | 1 | 0            rows-on-lanes band pass in place of the cooperative one (packed single boards whose
