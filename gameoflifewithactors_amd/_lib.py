@@ -62,6 +62,21 @@ class Strip(ctypes.Structure):
 
 
 _lib = None
+# Objects that keep the loaded CDLL and may call it later (open Board handles, strips.HipEngine): unload() refuses
+# while any is alive, since a call through a dlclosed library jumps into unmapped code
+import weakref  # noqa: E402
+
+_holders: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def hold(obj) -> None:
+    """Register `obj` as a user of the loaded library until release(obj) or its collection."""
+    _holders.add(obj)
+
+
+def release(obj) -> None:
+    _holders.discard(obj)
+
 
 i64 = ctypes.c_int64
 u64 = ctypes.c_uint64
@@ -124,7 +139,14 @@ SIGNATURES = {
     "gol_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
     "gol_device_count": (ctypes.c_int, [ip]),
     "gol_step_timed": (ctypes.c_int, [vp, i64, ctypes.POINTER(ctypes.c_double)]),
+    # test and A/B knobs (csrc/gol_debug.h: internal, not part of the gol.h boundary)
+    "gol_debug_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64]),
+    "gol_debug_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
 }
+
+# Names gol_debug_set_option / gol_debug_get_option take (csrc/gol_debug.h); Board.set_option routes them there.
+DEBUG_OPTIONS = frozenset({"coop_epoch", "coop_spin_limit", "coop_r", "resident_threads", "coop_launch",
+                           "lanes_launches"})
 
 
 def _elf_sections(data: bytes, base: int = 0):
@@ -264,10 +286,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
 def unload() -> None:
     """dlclose libgol_hip.so now, while the HIP runtime -- and a profiler attached to it -- is still alive, so its
     device code is unregistered here and not in the process-exit destructors (DESIGN.md 6 "Exit under rocprofv3").
-    Close every board first.  load() maps it again afterwards."""
+    Close every board first: GolError while any Board or strip engine that holds the library is alive.  load()
+    maps it again afterwards."""
     global _lib
     if _lib is None:
         return
+    if len(_holders):
+        raise GolError(f"unload: {len(_holders)} board(s) / engine(s) still hold libgol_hip.so; close them first")
     import _ctypes
 
     handle = _lib._handle

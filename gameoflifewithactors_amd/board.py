@@ -50,6 +50,7 @@ class Board:
             check(self._lib.gol_create_ex(width, height, boundary, num_gpus, tblock_k, ilv, ctypes.byref(h)),
                   "gol_create")
         self._h = h
+        _lib.hold(self)
         self.width, self.height, self.boundary = width, height, boundary
         try:
             for name, value in (options or {}).items():
@@ -63,6 +64,7 @@ class Board:
         if getattr(self, "_h", None) is not None and self._h.value:
             check(self._lib.gol_destroy(self._h), "gol_destroy")
             self._h = None
+            _lib.release(self)
 
     def __enter__(self) -> "Board":
         return self
@@ -155,13 +157,16 @@ class Board:
 
     # ---------------------------------------------------------------- options
     def set_option(self, name: str, value: int) -> "Board":
-        """Per-board path / tuning option (gol_set_option, include/gol/gol.h lists the names)."""
-        check(self._lib.gol_set_option(self._h, name.encode(), int(value)), f"gol_set_option({name})")
+        """Per-board path / tuning option (gol_set_option, include/gol/gol.h lists the names).  The test and A/B
+        knobs of csrc/gol_debug.h (_lib.DEBUG_OPTIONS) go to gol_debug_set_option."""
+        fn = "gol_debug_set_option" if name in _lib.DEBUG_OPTIONS else "gol_set_option"
+        check(getattr(self._lib, fn)(self._h, name.encode(), int(value)), f"{fn}({name})")
         return self
 
     def get_option(self, name: str) -> int:
+        fn = "gol_debug_get_option" if name in _lib.DEBUG_OPTIONS else "gol_get_option"
         v = ctypes.c_int64()
-        check(self._lib.gol_get_option(self._h, name.encode(), ctypes.byref(v)), f"gol_get_option({name})")
+        check(getattr(self._lib, fn)(self._h, name.encode(), ctypes.byref(v)), f"{fn}({name})")
         return v.value
 
     # ---------------------------------------------------------------- stepping

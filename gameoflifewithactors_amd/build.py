@@ -19,6 +19,7 @@ HEADERS = [
     os.path.join(CSRC, "gol_layout.h"),
     os.path.join(CSRC, "gol_internal.h"),
     os.path.join(CSRC, "gol_multi.h"),
+    os.path.join(CSRC, "gol_debug.h"),
     os.path.join(ROOT, "include", "gol", "gol.h"),
 ]
 ARCH = "gfx950"

@@ -15,12 +15,19 @@
 #include <vector>
 
 #include "../../include/gol/gol.h"
+#include "gol_debug.h"
 #include "gol_internal.h"
 #include "gol_multi.h"
 
 namespace {
 
 thread_local std::string g_last_error;
+
+// The test and A/B knobs of gol_debug.h (gol_debug_set_option), refused by gol_set_option with a pointer there.
+bool is_debug_option(const std::string& n) {
+    return n == "coop_epoch" || n == "coop_spin_limit" || n == "coop_r" || n == "resident_threads" ||
+           n == "coop_launch" || n == "lanes_launches";
+}
 
 // Every board call runs on the board's device whatever device the calling thread has current (staging
 // buffers are allocated on the current device), and restores the caller's device afterwards.
@@ -482,9 +489,9 @@ int lanes_depth(const gol_board* b) {
 bool use_lanes(const gol_board* b, int64_t gens) {
     if (!b->opt.lanes || !b->opt.coop || !b->packed || b->multi) return false;
     if (b->opt.lanes == 2 && !lanes_by_size(b->W, b->H)) return false;
-    gol::LanesPlan p;
+    // every band resident at once: a tall narrow board plans more bands than the device holds
     return gens >= 2 * lanes_depth(b) && b->W * b->H <= b->opt.coop_max_cells &&
-           gol::lanes_plan(b->W, b->H, lanes_depth(b), b->opt.lanes_m, &p);
+           gol::lanes_fits(b->W, b->H, lanes_depth(b), b->opt.lanes_m, b->ilv, b->boundary == GOL_BOUNDED);
 }
 
 bool use_coop(const gol_board* b) {
@@ -1433,35 +1440,73 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         if (value < 0 || value > 2) return fail(GOL_ERR_INVALID, "ragged_ring must be 0, 1 (by size) or 2");
         o.ragged_ring = (int)value;
     }
-    else if (n == "coop_r") {
-        if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
-        o.coop_r = (int)value;
-    } else if (n == "coop_poll_delay") {
+    else if (n == "coop_poll_delay") {
         if (value < -1 || value > 4096) return fail(GOL_ERR_INVALID, "coop_poll_delay must be -1 (auto) or 0..4096");
         o.coop_poll_delay = (int)value;
-    } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
-    else if (n == "lanes") {
+    } else if (n == "lanes") {
         if (value < 0 || value > 2) return fail(GOL_ERR_INVALID, "lanes must be 0, 1 or 2 (by size)");
         o.lanes = (int)value;
     }
-    else if (n == "coop_launch") o.coop_launch = value != 0;
     else if (n == "lanes_m") {
         if (value != 0 && value != 3 && value != 5 && value != 9 && value != 17)
             return fail(GOL_ERR_INVALID, "lanes_m must be 0, 3, 5, 9 or 17");
         o.lanes_m = (int)value;
-    }
+    } else if (is_debug_option(n))
+        return fail(GOL_ERR_INVALID, "'" + n + "' is a test knob (gol_debug_set_option, csrc/gol_debug.h), not a board option");
+    else
+        return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
+    // a multi-part board runs every strip launch with the streaming options (the other passes never run there)
+    if (b->multi) b->multi->set_stream_options(o.split, o.seg_rows, o.seam);
+    return GOL_OK;
+}
+
+// Test and A/B knobs (csrc/gol_debug.h; VERDICT round 4 item 3: kept out of gol.h's option list).
+int gol_debug_set_option(gol_board* b, const char* name, int64_t value) {
+    if (int rc = check_board(b)) return rc;
+    if (!name) return fail(GOL_ERR_INVALID, "null option name");
+    std::lock_guard<std::mutex> g(b->mu);
+    const std::string n(name);
+    BoardOptions& o = b->opt;
+    if (n == "coop_r") {
+        if (value < 1 || value > 8) return fail(GOL_ERR_INVALID, "coop_r must be 1..8");
+        o.coop_r = (int)value;
+    } else if (n == "coop_spin_limit") o.coop_spin_limit = value < 0 ? 0 : value;
+    else if (n == "coop_launch") o.coop_launch = value != 0;
     else if (n == "resident_threads") {
         if (value != 256 && value != 1024) return fail(GOL_ERR_INVALID, "resident_threads must be 256 or 1024");
         o.resident_threads = (int)value;
     } else if (n == "coop_epoch") {
-        // the epoch of the last cooperative launch, so the next one runs at value + 1: tests run the 16-bit wrap
-        // (and the clear of the granules it needs) early.  Only meaningful once the exchange buffer exists.
+        // the epoch of the last persistent launch, so the next one runs at value + 1: tests run the 16-bit wrap early.
+        // The granules are cleared with it: the buffer may hold granules of any earlier
+        // epoch, among them value + 1's own block 0 of parity 0, which would otherwise match the next launch's first
+        // poll and hand it stale halo rows.
         if (value < 0 || value > 0xffff) return fail(GOL_ERR_INVALID, "coop_epoch must be 0..65535");
-        if (b->coop_xch) b->coop_epoch = (unsigned)value;
-    } else
-        return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
-    // a multi-part board runs every strip launch with the streaming options (the other passes never run there)
-    if (b->multi) b->multi->set_stream_options(o.split, o.seg_rows, o.seam);
+        if (b->coop_xch) {
+            DeviceGuard dg(b->device);
+            GOL_HIP(hipMemsetAsync(b->coop_xch, 0, (size_t)b->coop_xch_words * sizeof(uint32_t), b->stream));
+            b->coop_epoch = (unsigned)value;
+        }
+    } else if (n == "lanes_launches")
+        return fail(GOL_ERR_INVALID, "lanes_launches is read-only");
+    else
+        return fail(GOL_ERR_INVALID, "unknown debug option '" + n + "'");
+    return GOL_OK;
+}
+
+int gol_debug_get_option(gol_board* b, const char* name, int64_t* value) {
+    if (int rc = check_board(b)) return rc;
+    if (!name || !value) return fail(GOL_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(b->mu);
+    const std::string n(name);
+    const BoardOptions& o = b->opt;
+    if (n == "coop_r") *value = o.coop_r;
+    else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
+    else if (n == "coop_launch") *value = o.coop_launch;
+    else if (n == "resident_threads") *value = o.resident_threads;
+    else if (n == "coop_epoch") *value = b->coop_epoch;
+    else if (n == "lanes_launches") *value = b->lanes_launches;
+    else
+        return fail(GOL_ERR_INVALID, "unknown debug option '" + n + "'");
     return GOL_OK;
 }
 
@@ -1481,16 +1526,12 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "seam") *value = o.seam;
     else if (n == "ragged_stream") *value = o.ragged_stream;
     else if (n == "ragged_ring") *value = o.ragged_ring;
-    else if (n == "coop_r") *value = o.coop_r;
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
-    else if (n == "coop_spin_limit") *value = o.coop_spin_limit;
     else if (n == "lanes") *value = o.lanes;
-    else if (n == "coop_launch") *value = o.coop_launch;
     else if (n == "lanes_m") *value = o.lanes_m;
-    else if (n == "lanes_launches") *value = b->lanes_launches;
-    else if (n == "resident_threads") *value = o.resident_threads;
-    else if (n == "coop_epoch") *value = b->coop_epoch;
     else if (n == "transport") *value = b->multi ? b->multi->transport() : GOL_TRANSPORT_NONE;
+    else if (is_debug_option(n))
+        return fail(GOL_ERR_INVALID, "'" + n + "' is a test knob (gol_debug_get_option, csrc/gol_debug.h), not a board option");
     else
         return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
     return GOL_OK;

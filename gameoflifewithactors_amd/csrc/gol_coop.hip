@@ -443,16 +443,6 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     }
 }
 
-int coop_cus() {
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 0;
-        return n;
-    }();
-    return cus;
-}
-
 constexpr int kRows[] = {1, 2, 3, 4, 6, 8};  // rows per wave instantiated
 
 template <int M, int R, int LAY>
@@ -499,7 +489,7 @@ int coop_m(int64_t nw) {
 // neighbour rows; 1 by default).
 bool coop_plan(int64_t W, int64_t H, int k, int* nwg, int* B, int* R, int min_rows) {
     if (min_rows < 1 || min_rows > 8) min_rows = 1;
-    const int cus = coop_cus();
+    const int cus = device_cus();
     if (cus <= 0 || W < 32 || W % 32 || H < 3 || k < 1 || !coop_m(W / 32)) return false;
     // balanced bands of >= k rows each (a k-row halo then comes from ONE neighbour band), one per CU at most
     int64_t n = H / k < cus ? H / k : cus;
@@ -558,24 +548,45 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     if (!fn) return hipErrorInvalidValue;
     const size_t need = (size_t)2 * kSlots * kSlotRows * M * 64 * 4;
     const size_t lds = need > (size_t)kMinLds ? need : (size_t)kMinLds;
-    {  // the LDS attribute once per kernel (a host call per launch otherwise)
-        static std::mutex mu;
-        static std::vector<const void*> done;
-        std::lock_guard<std::mutex> lock(mu);
-        if (std::find(done.begin(), done.end(), fn) == done.end()) {
-            const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            done.push_back(fn);
-        }
-    }
+    if (hipError_t e = set_max_dynamic_lds(fn, (int)lds)) return e;
     void* args[] = {&a};
     return launch_persistent(fn, (unsigned)nwg, kThreads, args, lds, s, !tune.plain_launch);
 }
 
-hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, void** args, size_t lds, hipStream_t s,
-                             bool cooperative) {
-    if (cooperative) return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s);
+// ---- device-keyed host state of the persistent passes (every cache keyed by device, so a process
+// driving boards on several GPUs -- or GPUs of different CU counts -- never uses another device's answer)
+
+int device_cus() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> known;  // (device, CUs)
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto& k : known)
+        if (k.first == dev) return k.second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    known.emplace_back(dev, n);
+    return n;
+}
+
+hipError_t set_max_dynamic_lds(const void* fn, int bytes) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    static std::mutex mu;
+    static std::vector<std::pair<int, const void*>> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (std::find(done.begin(), done.end(), std::make_pair(dev, fn)) != done.end()) return hipSuccess;
+    if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) return e;
+    done.emplace_back(dev, fn);
+    return hipSuccess;
+}
+
+int64_t persistent_capacity(const void* fn, unsigned threads, size_t lds) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
     struct Fit {
+        int dev;
         const void* fn;
         unsigned threads;
         size_t lds;
@@ -583,23 +594,63 @@ hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, vo
     };
     static std::mutex mu;
     static std::vector<Fit> fits;
-    int64_t resident = -1;
+    std::lock_guard<std::mutex> lock(mu);
+    for (const Fit& f : fits)
+        if (f.dev == dev && f.fn == fn && f.threads == threads && f.lds == lds) return f.resident;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)threads, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return -1;
+    const int64_t resident = (int64_t)per_cu * cus;
+    fits.push_back({dev, fn, threads, lds, resident});
+    return resident;
+}
+
+// Persistent passes of every board in the process run one at a time per device.  Each
+// launch waits on the device's last persistent launch (hipStreamWaitEvent) and becomes the new last one: two grids
+// whose bands spin on each other are then never resident together, so two handles stepping mid-size boards from two
+// threads on their own streams cannot split the CUs between them and starve both (gol.h: separate handles are
+// independent).  A per-device mutex orders the wait, the launch and the record.  Ordinary launches (the streaming
+// pass, I/O kernels) of other streams still share the device; they end on their own, so a persistent grid waits for
+// CUs they hold at most for their duration (the spin limit is ~2 s).
+namespace {
+struct DeviceSerial {
+    int dev;
+    std::mutex* mu;
+    hipEvent_t last;
+};
+}  // namespace
+
+hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, void** args, size_t lds, hipStream_t s,
+                             bool cooperative) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    const int64_t resident = persistent_capacity(fn, threads, lds);
+    if (resident < 0) return hipErrorInvalidValue;
+    if ((int64_t)grid > resident) return hipErrorCooperativeLaunchTooLarge;
+    static std::mutex table_mu;
+    static std::vector<DeviceSerial> table;  // entries are never removed (one per device)
+    std::mutex* mu = nullptr;
+    hipEvent_t last = nullptr;  // per device, both fixed once created (the table itself may grow)
     {
-        std::lock_guard<std::mutex> lock(mu);
-        for (const Fit& f : fits)
-            if (f.fn == fn && f.threads == threads && f.lds == lds) resident = f.resident;
-        if (resident < 0) {
-            int per_cu = 0, dev = 0, cus = 0;
-            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)threads, lds);
-            if (e == hipSuccess) e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e != hipSuccess) return e;
-            resident = (int64_t)per_cu * cus;
-            fits.push_back({fn, threads, lds, resident});
+        std::lock_guard<std::mutex> lock(table_mu);
+        for (const DeviceSerial& d : table)
+            if (d.dev == dev) {
+                mu = d.mu;
+                last = d.last;
+            }
+        if (!mu) {
+            if (hipError_t e = hipEventCreateWithFlags(&last, hipEventDisableTiming)) return e;
+            mu = new std::mutex;
+            table.push_back({dev, mu, last});
         }
     }
-    if ((int64_t)grid > resident) return hipErrorCooperativeLaunchTooLarge;
-    return hipLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, s);
+    std::lock_guard<std::mutex> lock(*mu);
+    if (hipError_t e = hipStreamWaitEvent(s, last, 0)) return e;  // an unrecorded event: no wait
+    const hipError_t e = cooperative ? hipLaunchCooperativeKernel(fn, dim3(grid), dim3(threads), args, (unsigned)lds, s)
+                                     : hipLaunchKernel(fn, dim3(grid), dim3(threads), args, lds, s);
+    if (e != hipSuccess) return e;
+    return hipEventRecord(last, s);
 }
 
 }  // namespace gol

@@ -128,8 +128,16 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
 // check against the occupancy API (hipErrorCooperativeLaunchTooLarge when the grid cannot be resident).  The plain
 // launch is the default (board option "coop_launch"): the runtime's cooperative-launch state is torn down at process
 // exit after a profiler's (rocprofv3 --kernel-trace) and faulted there (DESIGN.md 6 "Exit under rocprofv3").
+// Persistent launches of all boards are serialised per device (each waits on the device's previous one), so two
+// such grids are never resident together.
 hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, void** args, size_t lds, hipStream_t s,
                              bool cooperative);
+// Workgroups of (fn, threads, lds) the current device holds at once (occupancy API x CUs; cached per device), -1 on
+// error; CUs of the current device (cached per device, 0 without one); the dynamic-LDS attribute once per
+// (device, kernel).
+int64_t persistent_capacity(const void* fn, unsigned threads, size_t lds);
+int device_cus();
+hipError_t set_max_dynamic_lds(const void* fn, int bytes);
 
 // ---- gol_lanes.hip: rows-on-lanes band pass (a wave owns all rows of a band window of 64 (m - 1) columns and
 // steps it k generations alone), packed boards of any interleave, W a multiple of 64 (m - 1), k <= 16
@@ -142,6 +150,9 @@ struct LanesPlan {
 // m_opt: 0 = by width (3 up to 1024 columns, else 9 when W % 512 == 0, else 5), or 3 / 5 / 9 / 17
 bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out);
 int64_t lanes_xch_words(const LanesPlan& p, int k);
+// The plan's bands can all be resident at once on the current device (a tall narrow board plans more
+// bands than the device holds; such a board takes the cooperative or the streaming pass instead)
+bool lanes_fits(int64_t W, int64_t H, int k, int m_opt, int ilv, bool bounded);
 // as launch_coop_pass (gens <= 65535 per launch, epoch-tagged granules in xch, *err on a timed-out wait)
 hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                              int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,

@@ -398,6 +398,30 @@ bool lanes_plan(int64_t W, int64_t H, int k, int m_opt, LanesPlan* out) {
 
 int64_t lanes_xch_words(const LanesPlan& p, int k) { return (int64_t)2 * p.nb * 2 * k * p.nx * 2 * p.m * 2; }
 
+namespace {
+// LDS of one band: its plain board rows and the edge slots, raised so that at most ceil(nb / CUs) workgroups share a CU
+// (the dispatcher would otherwise stack two bands on one CU while another idles, and every band waits on the slowest)
+size_t lanes_lds(const LanesPlan& p, int64_t W) {
+    size_t lds = ((size_t)kWinRows * (size_t)(W / 32) + (size_t)2 * p.nx * 64) * sizeof(uint32_t);
+    const int cus = device_cus();
+    if (cus > 0) {
+        const size_t per_cu = ((size_t)p.nb + cus - 1) / cus;
+        const size_t floor = (size_t)160 * 1024 / (per_cu + 1) + 1024;
+        if (floor * per_cu <= (size_t)160 * 1024 && floor > lds) lds = floor;
+    }
+    return lds;
+}
+}  // namespace
+
+bool lanes_fits(int64_t W, int64_t H, int k, int m_opt, int ilv, bool bounded) {
+    LanesPlan p;
+    if (!lanes_plan(W, H, k, m_opt, &p) || (W / 32) % ilv) return false;
+    const void* fn = lane_kernel(p.m, ilv, bounded);
+    if (!fn || set_max_dynamic_lds(fn, 96 * 1024) != hipSuccess) return false;
+    const int64_t resident = persistent_capacity(fn, (unsigned)(64 * p.nx), lanes_lds(p, W));
+    return resident >= p.nb;
+}
+
 hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64_t H, int64_t pitch, int ilv, int k,
                              int64_t gens, bool bounded, unsigned epoch, int* err, uint32_t* xch, int64_t xch_words,
                              hipStream_t s, int m_opt, const CoopTuning& tune) {
@@ -423,30 +447,8 @@ hipError_t launch_lanes_pass(const uint32_t* src, uint32_t* dst, int64_t W, int6
     a.poll_delay = tune.poll_delay >= 0 ? tune.poll_delay : 8;
     a.spin_limit = tune.spin_limit ? tune.spin_limit : kLaneSpinLimit;
     a.err = err;
-    size_t lds = ((size_t)kWinRows * a.nw + (size_t)2 * p.nx * 64) * sizeof(uint32_t);
-    // spread the bands evenly: an LDS request that admits at most ceil(nb / CUs) workgroups per CU (the dispatcher
-    // would otherwise stack two bands on one CU while another idles, and every band waits on the slowest)
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 0;
-        return n;
-    }();
-    if (cus > 0) {
-        const size_t per_cu = ((size_t)p.nb + cus - 1) / cus;
-        const size_t floor = (size_t)160 * 1024 / (per_cu + 1) + 1024;
-        if (floor * per_cu <= (size_t)160 * 1024 && floor > lds) lds = floor;
-    }
-    {  // the LDS attribute once per kernel
-        static std::mutex mu;
-        static std::vector<const void*> done;
-        std::lock_guard<std::mutex> lock(mu);
-        if (std::find(done.begin(), done.end(), fn) == done.end()) {
-            const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            if (e != hipSuccess) return e;
-            done.push_back(fn);
-        }
-    }
+    const size_t lds = lanes_lds(p, W);
+    if (hipError_t e = set_max_dynamic_lds(fn, 96 * 1024)) return e;
     void* args[] = {&a};
     return launch_persistent(fn, (unsigned)p.nb, (unsigned)(64 * p.nx), args, lds, s, !tune.plain_launch);
 }

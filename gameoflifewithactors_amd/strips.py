@@ -69,6 +69,7 @@ class HipEngine:
 
     def __init__(self, device: torch.device):
         self.lib = _lib.load()
+        _lib.hold(self)  # _lib.unload() refuses while this engine can still call the library
         self.device = device
 
     def ilv_for(self, width: int) -> int:

@@ -185,18 +185,17 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *                                words (0: the per-generation byte step)
  *   "coop_poll_delay" -1 | 0..4096  s_sleep periods before a hand-off's first poll (-1: 0 on cooperative-pass rows of
  *                                <= 2048 cells, else 8)
- *   "coop_r" 1..8, "resident_threads" 1024 | 256: A/B experiments
- *   "coop_spin_limit" 0 | n      polls before a hand-off wait gives up (0: ~2 s; tests force a timeout)
- *   "coop_epoch" n               tests: the tag epoch of the last cooperative launch (the next runs at n + 1)
  *   "lanes" 2 | 1 | 0            rows-on-lanes band pass in place of the cooperative one (packed single boards whose
  *                                width splits into 128/256/512/1024-column windows, coop_k <= 10, calls of >= 2 k
- *                                generations): 2 = on the sizes it measured faster (rows of <= 1024
- *                                cells; 8192 wide up to 4096 rows), 1 = wherever it applies, 0 = never
+ *                                generations, every band resident at once): 2 = on the sizes it
+ *                                measured faster (rows of <= 1024 cells; 8192 wide up to 4096 rows), 1 = wherever it
+ *                                applies, 0 = never
  *   "lanes_m" 0 | 3 | 5 | 9 | 17 its words per lane and half-row (0: 3 up to 1024 columns, else 9 when W % 512 == 0)
- *   "coop_launch" 0 | 1          the persistent passes by hipLaunchKernel after a residency check (0), or by
- *                                hipLaunchCooperativeKernel (1; DESIGN.md 6 "Exit under rocprofv3")
- *   "lanes_launches" (read-only) launches of that pass on this board (tests)
- * Unknown names and out-of-range values return GOL_ERR_INVALID.  Results are bit-identical for every setting. */
+ * Unknown names and out-of-range values return GOL_ERR_INVALID.  Results are bit-identical for every setting.
+ * (Test and A/B knobs -- spin limits, tag epochs, launch API -- are not board options: they live behind
+ * gol_debug_set_option in the library's internal header csrc/gol_debug.h.)
+ * The persistent passes (cooperative, rows-on-lanes) of all boards of a process are serialised per device, so two
+ * handles stepping at once from two threads never split the CUs between two such grids. */
 int gol_set_option(gol_board* b, const char* name, int64_t value);
 int gol_get_option(gol_board* b, const char* name, int64_t* value);
 

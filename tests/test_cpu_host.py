@@ -69,7 +69,14 @@ def test_library_unloads_and_reloads():
     code = ("import sys; sys.path.insert(0, %r)\n"
             "from gameoflifewithactors_amd import _lib\n"
             "_lib.load(); _lib.unload(); assert _lib._lib is None\n"
-            "print(_lib.load().gol_version().decode()); _lib.unload()\n") % root
+            "print(_lib.load().gol_version().decode()); _lib.unload()\n"
+            # refused while an object that may call the library is alive, allowed after its release
+            "class H: pass\n"
+            "h = H(); _lib.load(); _lib.hold(h)\n"
+            "try:\n    _lib.unload(); raise SystemExit('unload with a live holder')\n"
+            "except _lib.GolError: pass\n"
+            "assert _lib._lib is not None\n"
+            "_lib.release(h); _lib.unload(); assert _lib._lib is None\n") % root
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "gfx950" in r.stdout

@@ -106,6 +106,43 @@ def test_coop_epoch_wrap(gol, oracle):
         np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, done, 0))
 
 
+@pytest.mark.parametrize("lanes", [0, 1])
+def test_epoch_set_back_reuses_no_stale_granule(gol, oracle, lanes):
+    """the debug knob "coop_epoch" set to the last launch's epoch - 1 makes the next launch
+    run at the SAME epoch as the last one, whose granules (block 0 of parity 0 included) are still in the exchange
+    buffer.  Setting the epoch clears the buffer, so the launch must poll for its own neighbours' data and stay
+    exact.  4096^2, 16 generations after the reuse, on the cooperative and the rows-on-lanes pass."""
+    b0 = _rand(4096, 4096, 95)
+    with gol.Board(4096, 4096, 0, options={"coop": 1, "lanes": lanes}) as b:
+        b.set_cells(b0)
+        b.step(16)
+        last = b.get_option("coop_epoch")
+        b.set_option("coop_epoch", last - 1)
+        b.step(16)
+        assert b.get_option("coop_epoch") == last
+        if lanes:
+            assert b.get_option("lanes_launches") == 2
+        np.testing.assert_array_equal(b.get_cells(), oracle.c_run(b0, 32, 0))
+
+
+def test_debug_knobs_are_not_board_options(gol):
+    """gol.h's option list holds only product settings: the test knobs are refused by gol_set_option /
+    gol_get_option and reached through gol_debug_set_option (csrc/gol_debug.h)."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    with gol.Board(1024, 1024, 0) as b:
+        v = ctypes.c_int64()
+        for name in sorted(_lib.DEBUG_OPTIONS):
+            assert lib.gol_set_option(b._h, name.encode(), 1) == _lib.GOL_ERR_INVALID, name
+            assert lib.gol_get_option(b._h, name.encode(), ctypes.byref(v)) == _lib.GOL_ERR_INVALID, name
+            assert lib.gol_debug_get_option(b._h, name.encode(), ctypes.byref(v)) == _lib.GOL_OK, name
+        for name in ("coop", "coop_k", "lanes", "split"):
+            assert lib.gol_debug_set_option(b._h, name.encode(), 0) == _lib.GOL_ERR_INVALID, name
+
+
 def test_coop_timeout_reported_on_every_readback(gol, oracle):
     """A band hand-off wait that times out (forced here: a spin limit of one poll, while the neighbour band has not
     published yet) leaves a wrong board.  Every readback and gol_synchronize must report it (GOL_ERR_HIP), the

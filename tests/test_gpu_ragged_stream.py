@@ -116,3 +116,16 @@ def test_ragged_stream_large_board(gol, oracle):
     win = np.roll(b0, 100, axis=1)[5000 - gens:5200 + gens, :200 + gens]
     sub = oracle.c_run(np.ascontiguousarray(np.pad(win, 0)), gens, 1)
     np.testing.assert_array_equal(np.roll(got, 100, axis=1)[5000:5200, gens:200], sub[gens:200 + gens, gens:200])
+
+
+@pytest.mark.parametrize("calls", [[100], [32, 32, 32, 4, 32]])
+def test_ring_refresh_long_ring_state(gol, oracle, calls):
+    """torus ring rows kept in one ring state past 64 generations, so the refresh of the copies at both
+    ends of every row (gol_ring_refresh, whenever ring_age + k would pass the 64 copied cells) runs between passes --
+    one 100-generation call, and 32-generation calls whose state stays in the ring rows between them (the 4-generation
+    call is the streaming pass too: >= 4 generations).  Against the oracle and the ilv-1 rows ("ragged_ring" 0)."""
+    w, h = 8209, 70
+    b0 = _rand(h, w, 808)
+    want = oracle.c_run(b0, sum(calls), 0)
+    np.testing.assert_array_equal(_run(gol, b0, 0, calls, stream=True, ring=2), want)
+    np.testing.assert_array_equal(_run(gol, b0, 0, calls, stream=True, ring=0), want)
