@@ -51,6 +51,21 @@ constexpr int kSlotRows = GOL_COOP_XH ? 4 : 2;  // LDS words per lane and word o
 // waves), so every wave reads its neighbours' slots without a branch
 constexpr int kSlots = kWaves + 2;
 
+// GOL_COOP_STAMP (diagnostic builds only, never shipped): per band, wave and block, the time (s_memrealtime, 100 MHz)
+// right after the wave issued its hand-off stores for the block, and right after its poll for the block's halo rows
+// returned; gol_debug_coop_stamps() copies them out (tools/coop_stamps.py splits a block into compute and hand-off)
+#ifndef GOL_COOP_STAMP
+#define GOL_COOP_STAMP 0
+#endif
+#if GOL_COOP_STAMP
+constexpr int kStampBands = 256, kStampBlocks = 128;
+__device__ unsigned long long g_coop_stamps[kStampBands * kWaves * kStampBlocks * 2];
+__device__ __forceinline__ void coop_stamp(int band, int wv, int blk, int what) {
+    if (band < kStampBands && blk < kStampBlocks && (threadIdx.x & 63) == 0)
+        g_coop_stamps[((band * kWaves + wv) * kStampBlocks + blk) * 2 + what] = __builtin_amdgcn_s_memrealtime();
+}
+#endif
+
 
 struct CoopArgs {
     const uint32_t* src;  // board at launch
@@ -312,6 +327,9 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                 failed = true;
             }
         }
+#if GOL_COOP_STAMP
+        coop_stamp(band, wv, blk, 1);
+#endif
         // k generations: generation j computes local rows [K - k + 1 + j, K + B + k - 1 - j).  The wave's own row
         // sums do not depend on the exchange: they are summed between publishing the edge rows and the barrier,
         // so the barrier wait and the LDS round trip overlap them.
@@ -429,6 +447,9 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                 st_granules<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
             }
         }
+#if GOL_COOP_STAMP
+        coop_stamp(band, wv, blk, 0);
+#endif
     }
     // ---- the band to the result buffer
     if (!lane_on) return;
@@ -654,3 +675,13 @@ hipError_t launch_persistent(const void* fn, unsigned grid, unsigned threads, vo
 }
 
 }  // namespace gol
+
+#if GOL_COOP_STAMP
+extern "C" int gol_debug_coop_stamps(unsigned long long* out, long long n) {
+    const long long cap = (long long)gol::kStampBands * gol::kWaves * gol::kStampBlocks * 2;
+    if (n > cap) n = cap;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gol::g_coop_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0
+               : -2;
+}
+#endif

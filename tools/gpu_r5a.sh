@@ -28,3 +28,5 @@ done
 cd $GRAFT_REPO_ROOT
 python3 tools/pmc_summary.py $O/pmc_coop --kernel gol_band_pass > $O/sq_coop.json && cat $O/sq_coop.json
 python3 tools/pmc_summary.py $O/pmc_l9 --kernel gol_lane_pass > $O/sq_l9.json && cat $O/sq_l9.json
+step stamps 300 python tools/coop_stamps.py --boards 4096x4096x0,2048x2048x0,4096x4096x1 --gens 1000
+cat $O/stamps.log
