@@ -84,6 +84,7 @@ struct CoopArgs {
     int* err;             // set to 1 by a timed-out wait
     int rag_lb;           // ragged rows (kLayRagged): bit of the last cell in the last word, (W - 1) & 31
     int rag_last;         // ragged rows: index of the last word that holds cells, ceil(W / 32) - 1
+    int xch_bytes;        // bytes of the exchange buffer (the granules' buffer descriptor)
 };
 
 // A lane's M words of one row as granules {word, tag}, write-through (8-byte sc1 stores)
@@ -148,6 +149,59 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
         if (src[i])
 #pragma unroll
             for (int t = 0; t < M; t++) w[i][t] = (uint32_t)v[i][t];
+    return true;
+}
+
+// GOL_COOP_G16 (A/B): a lane's granules in pairs, as 16-byte write-through stores and 16-byte sc1 polls (two {word,
+// tag} granules per access, each 8-byte half written by ONE store: MI355X_MICROARCH.md "Valid forms", R2 halves) --
+// half the hand-off's memory instructions at M = 2 and whole 1 KB runs per wave instruction
+// GOL_COOP_POSOFF (A/B): LDS slot addresses relative to the slot of the wave above (positive immediate offsets: one
+// address VALU per generation instead of five)
+#ifndef GOL_COOP_POSOFF
+#define GOL_COOP_POSOFF 0
+#endif
+#ifndef GOL_COOP_G16
+#define GOL_COOP_G16 0
+#endif
+constexpr int kAuxSc1 = 16;  // buffer instruction cache policy: sc1 (gfx950)
+typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
+template <int M>
+__device__ __forceinline__ void st_granules16(__amdgpu_buffer_rsrc_t xrs, int off, const uint32_t (&w)[M], unsigned tag) {
+#pragma unroll
+    for (int t = 0; t < M; t += 2) {
+        const u32x4c v = {w[t], tag, w[t + 1], tag};
+        __builtin_amdgcn_raw_buffer_store_b128(v, xrs, off + 8 * t, 0, kAuxSc1);
+    }
+}
+template <int M, int R>
+__device__ __forceinline__ bool ld_granules16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R], uint32_t (&w)[R][M],
+                                              unsigned tag, int delay, unsigned spin_limit) {
+    for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
+    u32x4c v[R][M / 2];
+    for (unsigned it = 0;; it++) {
+#pragma unroll
+        for (int i = 0; i < R; i++)
+#pragma unroll
+            for (int t = 0; t < M / 2; t++)
+                v[i][t] = off[i] >= 0 ? __builtin_amdgcn_raw_buffer_load_b128(xrs, off[i] + 16 * t, 0, kAuxSc1)
+                                      : u32x4c{0u, tag, 0u, tag};
+        bool miss = false;
+#pragma unroll
+        for (int i = 0; i < R; i++)
+#pragma unroll
+            for (int t = 0; t < M / 2; t++) miss = miss || v[i][t].y != tag || v[i][t].w != tag;
+        if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
+        if (it == spin_limit) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++)
+        if (off[i] >= 0)
+#pragma unroll
+            for (int t = 0; t < M / 2; t++) {
+                w[i][2 * t] = v[i][t].x;
+                w[i][2 * t + 1] = v[i][t].z;
+            }
     return true;
 }
 
@@ -267,6 +321,8 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         return a.xch + ((((int64_t)parity * a.nwg + b) * 2 + side) * K + i) * a.nw;
     };
     auto tag_of = [&](int blk) { return a.epoch << 16 | (unsigned)(blk + 1); };  // tag of block blk's granules
+    constexpr bool G16 = GOL_COOP_G16 && M % 2 == 0;
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.xch, (short)0, a.xch_bytes, 0x00020000);
 
     // ---- the band and its halo from the board (plain loads: the board buffers are not handed off in-kernel)
     uint32_t w[R][M];
@@ -321,8 +377,18 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
                                                                           __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
                 failed = true;
-            if (!failed && __builtin_amdgcn_ballot_w64(any) != 0 &&
-                !ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit)) {
+            bool got;
+            if constexpr (G16) {
+                int off[R];
+#pragma unroll
+                for (int i = 0; i < R; i++) off[i] = src[i] ? (int)((src[i] - a.xch) * 8) : -1;
+                got = failed || __builtin_amdgcn_ballot_w64(any) == 0 ||
+                      ld_granules16<M, R>(xrs, off, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
+            } else {
+                got = failed || __builtin_amdgcn_ballot_w64(any) == 0 ||
+                      ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
+            }
+            if (!got) {
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 failed = true;
             }
@@ -336,7 +402,15 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         for (int j = 0; j < k; j++) {
             const int gen = blk * K + j;  // generation of this launch
             const int par = gen & 1;      // alternates across blocks too: no barrier separates them
+#if GOL_COOP_POSOFF
+            // the slot of wave wv - 1 (slot index wv): this wave's reads and writes are all at positive constant
+            // offsets from it (one address per generation; the ds instructions' immediate offsets do the rest)
+            uint32_t* nb = xs + ((par * kSlots + wv) * kSlotRows * M) * 64 + lane;
+            auto SL = [&](int w_rel, int q, int t) -> uint32_t& { return nb[((w_rel * 4 + q) * M + t) * 64]; };
+#else
             uint32_t* slot = xs + (par * kSlots + 1) * kSlotRows * M * 64;  // slot[-1] and slot[kWaves] are zero
+            auto SL = [&](int w_rel, int q, int t) -> uint32_t& { return slot[(((wv - 1 + w_rel) * 4 + q) * M + t) * 64 + lane]; };
+#endif
             // (dead outside a bounded board at every generation: `dead` below)
             const int lo = K - k + 1 + j, hi = K + B + k - 1 - j;
             const bool active = r0 < hi && r0 + R > lo;  // wave-uniform: some of this wave's rows are produced
@@ -353,10 +427,10 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             }
 #pragma unroll
             for (int t = 0; t < M; t++) {
-                slot[((wv * 4 + 0) * M + t) * 64 + lane] = so[0][t];
-                slot[((wv * 4 + 1) * M + t) * 64 + lane] = co[0][t];
-                slot[((wv * 4 + 2) * M + t) * 64 + lane] = so[R - 1][t];
-                slot[((wv * 4 + 3) * M + t) * 64 + lane] = co[R - 1][t];
+                SL(1, 0, t) = so[0][t];
+                SL(1, 1, t) = co[0][t];
+                SL(1, 2, t) = so[R - 1][t];
+                SL(1, 3, t) = co[R - 1][t];
             }
             // the wave's interior rows need no neighbour: stepped while the edge sums travel through LDS
             if (active) {
@@ -376,10 +450,10 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             uint32_t sa[M], ca[M], sb[M], cb[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
-                sa[t] = slot[(((wv - 1) * 4 + 2) * M + t) * 64 + lane];
-                ca[t] = slot[(((wv - 1) * 4 + 3) * M + t) * 64 + lane];
-                sb[t] = slot[(((wv + 1) * 4 + 0) * M + t) * 64 + lane];
-                cb[t] = slot[(((wv + 1) * 4 + 1) * M + t) * 64 + lane];
+                sa[t] = SL(0, 2, t);
+                ca[t] = SL(0, 3, t);
+                sb[t] = SL(2, 0, t);
+                cb[t] = SL(2, 1, t);
             }
             constexpr int kEdgeRows = R > 1 ? 2 : 1;  // rows 0 and R - 1 (interior rows are done)
 #pragma unroll
@@ -397,6 +471,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
 #else
 #pragma unroll
             for (int t = 0; t < M; t++) {
+                uint32_t* slot = xs + (par * kSlots + 1) * kSlotRows * M * 64;
                 slot[((wv * 2 + 0) * M + t) * 64 + lane] = w[0][t];
                 slot[((wv * 2 + 1) * M + t) * 64 + lane] = w[R - 1][t];
             }
@@ -414,6 +489,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             uint32_t above[M], below[M];
 #pragma unroll
             for (int t = 0; t < M; t++) {
+                uint32_t* slot = xs + (par * kSlots + 1) * kSlotRows * M * 64;
                 above[t] = slot[(((wv - 1) * 2 + 1) * M + t) * 64 + lane];
                 below[t] = slot[(((wv + 1) * 2 + 0) * M + t) * 64 + lane];
             }
@@ -444,7 +520,10 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             for (int side = 0; side < 2; side++) {
                 const int e = side == 0 ? li - K : li - B;  // row index within the band's top / bottom K rows
                 if (e < 0 || e >= K || !lane_on) continue;
-                st_granules<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
+                if constexpr (G16)
+                    st_granules16<M>(xrs, (int)((xrow(par, band, side, e) + col - a.xch) * 8), w[i], tag_of(blk));
+                else
+                    st_granules<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
             }
         }
 #if GOL_COOP_STAMP
@@ -549,6 +628,7 @@ hipError_t launch_coop_pass(const uint32_t* src, uint32_t* dst, int64_t W, int64
     a.src = src;
     a.dst = dst;
     a.xch = reinterpret_cast<uint64_t*>(xch);
+    a.xch_bytes = (int)std::min<int64_t>(xch_words * 4, 0x7fffffff);
     a.pitch = pitch;
     a.nw = nw;
     a.nl = nw / M;
