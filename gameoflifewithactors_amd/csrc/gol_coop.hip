@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 namespace gol {
@@ -152,6 +153,17 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
     return true;
 }
 
+// GOL_COOP_PIPE (A/B): poll rounds kept in flight.  A round is a batch of 8-byte sc1 loads that returns after a
+// memory round trip (~0.5-1 us under load); with one round at a time a poll that just misses the neighbour's data costs
+// a second whole round trip, so the measured hop (profiles/r5/coop_stamps_a.log: 4096^2 median 1.45 / 1.88 us, p10
+// 0.9) is quantised by it.  Here NP rounds are in flight, issued `gap` s_sleep periods apart: a round is checked
+// while the later ones are still out, and a miss re-issues it at once.
+#ifndef GOL_COOP_PIPE
+#define GOL_COOP_PIPE 1
+#endif
+#ifndef GOL_COOP_PIPE_GAP
+#define GOL_COOP_PIPE_GAP 2
+#endif
 // GOL_COOP_G16 (A/B): a lane's granules in pairs, as 16-byte write-through stores and 16-byte sc1 polls (two {word,
 // tag} granules per access, each 8-byte half written by ONE store: MI355X_MICROARCH.md "Valid forms", R2 halves) --
 // half the hand-off's memory instructions at M = 2 and whole 1 KB runs per wave instruction
@@ -165,44 +177,114 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
 #endif
 constexpr int kAuxSc1 = 16;  // buffer instruction cache policy: sc1 (gfx950)
 typedef unsigned int u32x4c __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2c __attribute__((ext_vector_type(2)));
+// Granule accesses of a lane's M words: pairs {word, tag, word, tag} as 16-byte accesses (M even), or single 8-byte
+// {word, tag} granules (M = 1).  Buffer instructions with the sc1 policy: never flat (MI355X_MICROARCH.md "Valid
+// forms": global_/buffer_ sc1 loads to registers).
 template <int M>
-__device__ __forceinline__ void st_granules16(__amdgpu_buffer_rsrc_t xrs, int off, const uint32_t (&w)[M], unsigned tag) {
-#pragma unroll
-    for (int t = 0; t < M; t += 2) {
-        const u32x4c v = {w[t], tag, w[t + 1], tag};
-        __builtin_amdgcn_raw_buffer_store_b128(v, xrs, off + 8 * t, 0, kAuxSc1);
+struct Gran {
+    static constexpr int G = M % 2 == 0 ? 2 : 1;  // granules per access
+    static constexpr int N = M / G;               // accesses per row
+    using V = typename std::conditional<G == 2, u32x4c, u32x2c>::type;
+    __device__ __forceinline__ static V load(__amdgpu_buffer_rsrc_t r, int off) {
+        if constexpr (G == 2) return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1);
+        else return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1);
     }
+    // The stores are global_store ... sc1 written out: with the buffer form the compiler waited vmcnt(0) before
+    // reusing a store's data or offset registers (before the next granule store, and at the top of the first generation
+    // of every block), so every write-through store waited for the previous one's completion.  A global store reads its
+    // address and data registers at issue.  (Not counted by the compiler's wait-count pass: its waits on later loads
+    // only get more conservative.)
+    __device__ __forceinline__ static void store(uint64_t* p, const uint32_t* w, unsigned tag) {
+        if constexpr (G == 2) {
+            const u32x4c v = {w[0], tag, w[1], tag};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        } else {
+            const u32x2c v = {w[0], tag};
+            asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        }
+    }
+    __device__ __forceinline__ static bool miss(const V& v, unsigned tag) {
+        if constexpr (G == 2) return v.y != tag || v.w != tag;
+        else return v.y != tag;
+    }
+    __device__ __forceinline__ static void take(const V& v, uint32_t* w) {
+        w[0] = v.x;
+        if constexpr (G == 2) w[1] = v.z;
+    }
+};
+template <int M>
+__device__ __forceinline__ void st_granules16(uint64_t* p, const uint32_t (&w)[M], unsigned tag) {
+#pragma unroll
+    for (int t = 0; t < Gran<M>::N; t++) Gran<M>::store(p + Gran<M>::G * t, &w[Gran<M>::G * t], tag);
+}
+// Polls of ld_granules16: rows the lane does not need load from an offset past the descriptor's range (zero, no
+// memory access, no branch) and are ignored by the tag check.
+constexpr int kNoGranule = 0x7fffffff;
+template <int M, int R>
+__device__ __forceinline__ void issue16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R],
+                                        typename Gran<M>::V (&v)[R][Gran<M>::N]) {
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int t = 0; t < Gran<M>::N; t++)
+            v[i][t] = Gran<M>::load(xrs, off[i] == kNoGranule ? kNoGranule : off[i] + 8 * Gran<M>::G * t);
 }
 template <int M, int R>
+__device__ __forceinline__ bool hit16(const int (&off)[R], const typename Gran<M>::V (&v)[R][Gran<M>::N], unsigned tag) {
+    bool miss = false;
+#pragma unroll
+    for (int i = 0; i < R; i++)
+#pragma unroll
+        for (int t = 0; t < Gran<M>::N; t++) miss = miss || (off[i] != kNoGranule && Gran<M>::miss(v[i][t], tag));
+    return __builtin_amdgcn_ballot_w64(miss) == 0;  // wave-uniform
+}
+template <int M, int R>
+__device__ __forceinline__ void take16(const int (&off)[R], const typename Gran<M>::V (&v)[R][Gran<M>::N],
+                                       uint32_t (&w)[R][M]) {
+#pragma unroll
+    for (int i = 0; i < R; i++)
+        if (off[i] != kNoGranule)
+#pragma unroll
+            for (int t = 0; t < Gran<M>::N; t++) Gran<M>::take(v[i][t], &w[i][Gran<M>::G * t]);
+}
+// NP = 1: one poll round at a time; NP = 2: two rounds in flight (GOL_COOP_PIPE), `gap` s_sleep periods apart
+template <int M, int R, int NP>
 __device__ __forceinline__ bool ld_granules16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R], uint32_t (&w)[R][M],
                                               unsigned tag, int delay, unsigned spin_limit) {
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
-    u32x4c v[R][M / 2];
-    for (unsigned it = 0;; it++) {
-#pragma unroll
-        for (int i = 0; i < R; i++)
-#pragma unroll
-            for (int t = 0; t < M / 2; t++)
-                v[i][t] = off[i] >= 0 ? __builtin_amdgcn_raw_buffer_load_b128(xrs, off[i] + 16 * t, 0, kAuxSc1)
-                                      : u32x4c{0u, tag, 0u, tag};
-        bool miss = false;
-#pragma unroll
-        for (int i = 0; i < R; i++)
-#pragma unroll
-            for (int t = 0; t < M / 2; t++) miss = miss || v[i][t].y != tag || v[i][t].w != tag;
-        if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
-        if (it == spin_limit) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int i = 0; i < R; i++)
-        if (off[i] >= 0)
-#pragma unroll
-            for (int t = 0; t < M / 2; t++) {
-                w[i][2 * t] = v[i][t].x;
-                w[i][2 * t + 1] = v[i][t].z;
+    typename Gran<M>::V va[R][Gran<M>::N], vb[R][Gran<M>::N];
+    issue16<M, R>(xrs, off, va);
+    if constexpr (NP == 1) {
+        for (unsigned it = 0;; it++) {
+            if (hit16<M, R>(off, va, tag)) break;
+            if (it == spin_limit) return false;
+            __builtin_amdgcn_s_sleep(1);
+            issue16<M, R>(xrs, off, va);
+        }
+        take16<M, R>(off, va, w);
+        return true;
+    } else {
+        for (int s = 0; s < GOL_COOP_PIPE_GAP; s++) __builtin_amdgcn_s_sleep(1);
+        issue16<M, R>(xrs, off, vb);
+        for (unsigned it = 0;; it++) {
+            if (hit16<M, R>(off, va, tag)) {
+                take16<M, R>(off, va, w);
+                return true;
             }
-    return true;
+            if (it == spin_limit) return false;
+            for (int s = 0; s < GOL_COOP_PIPE_GAP; s++) __builtin_amdgcn_s_sleep(1);
+            issue16<M, R>(xrs, off, va);
+            asm volatile("" ::: "memory");  // the re-issued round stays in flight while the other one is checked
+            if (hit16<M, R>(off, vb, tag)) {
+                take16<M, R>(off, vb, w);
+                return true;
+            }
+            for (int s = 0; s < GOL_COOP_PIPE_GAP; s++) __builtin_amdgcn_s_sleep(1);
+            issue16<M, R>(xrs, off, vb);
+            asm volatile("" ::: "memory");
+        }
+    }
 }
 
 // Word of the lane to the left / right.  FULL (all 64 lanes hold words): DPP rotate on a torus, DPP shift with
@@ -321,7 +403,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
         return a.xch + ((((int64_t)parity * a.nwg + b) * 2 + side) * K + i) * a.nw;
     };
     auto tag_of = [&](int blk) { return a.epoch << 16 | (unsigned)(blk + 1); };  // tag of block blk's granules
-    constexpr bool G16 = GOL_COOP_G16 && M % 2 == 0;
+    constexpr bool G16 = GOL_COOP_G16 && (M % 2 == 0 || GOL_COOP_G16 > 1);  // 2: M = 1 too (8-byte buffer accesses)
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.xch, (short)0, a.xch_bytes, 0x00020000);
 
     // ---- the band and its halo from the board (plain loads: the board buffers are not handed off in-kernel)
@@ -374,16 +456,25 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             // lane and agreed by ballot, so it stays a vector load) the board is invalid: stop waiting, so a launch
             // with a non-resident band ends after about one spin limit instead of one per block.  No early exit:
             // every wave still meets the generation barriers.
-            if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
-                failed = true;
+            // G16: only the waves that wait read it -- its load's wait (vmcnt counts stores) would hold a publishing
+            // wave at the top of every block until its own write-through granule stores had completed
+            if (!G16 || __builtin_amdgcn_ballot_w64(any) != 0)
+                if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
+                    failed = true;
             bool got;
             if constexpr (G16) {
                 int off[R];
 #pragma unroll
-                for (int i = 0; i < R; i++) off[i] = src[i] ? (int)((src[i] - a.xch) * 8) : -1;
-                got = failed || __builtin_amdgcn_ballot_w64(any) == 0 ||
-                      ld_granules16<M, R>(xrs, off, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
+                for (int i = 0; i < R; i++) off[i] = src[i] ? (int)((src[i] - a.xch) * 8) : kNoGranule;
+                got = true;
+                if (!failed && __builtin_amdgcn_ballot_w64(any) != 0) {
+                    got = ld_granules16<M, R, GOL_COOP_PIPE>(xrs, off, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
+                    // the polled rounds have all returned (the tag checks waited for them); saying so here keeps the
+                    // wait-count pass from assuming poll loads in flight at the granule stores and generation loop
+                    // below, where a vmcnt(0) would also wait for this wave's write-through stores
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                }
             } else {
                 got = failed || __builtin_amdgcn_ballot_w64(any) == 0 ||
                       ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
@@ -521,7 +612,7 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                 const int e = side == 0 ? li - K : li - B;  // row index within the band's top / bottom K rows
                 if (e < 0 || e >= K || !lane_on) continue;
                 if constexpr (G16)
-                    st_granules16<M>(xrs, (int)((xrow(par, band, side, e) + col - a.xch) * 8), w[i], tag_of(blk));
+                    st_granules16<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
                 else
                     st_granules<M>(xrow(par, band, side, e) + col, w[i], tag_of(blk));
             }
