@@ -224,6 +224,8 @@ struct BoardOptions {
     int64_t resident_max_cells = -1;          // "resident_max_cells": LDS-resident cut-over (-1 = per layout)
     bool wave_resident = true;                // "wave_resident": single-wave pass for boards <= 128 x 256
     int32_t split = 0;                        // "split": streaming pair split, 1/65536 (0 = engine, < 0 = off)
+    int32_t split2 = 0;                       // "split2": three-wave groups, the middle wave's share of the two
+                                              // younger waves' rows, 1/65536 (0 = engine)
     int64_t seg_rows = 0;                     // "seg_rows": streaming rows per wave segment (0 = planned)
     int seam = 0;                             // "seam": torus seam strips (0 = where they apply, -1 = off)
     bool ragged_stream = true;                // "ragged_stream": ragged boards beyond the cooperative pass stream
@@ -298,6 +300,7 @@ struct gol_board {
         a.seg = 0;
         a.ilv = ilv;
         a.split_opt = opt.split;
+        a.split2_opt = opt.split2;
         a.seg_opt = opt.seg_rows;
         a.seam_opt = opt.seam;
         return a;
@@ -556,10 +559,11 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     }
     gol::CoopTuning tune;
     tune.min_rows = b->opt.coop_r;
-    // first-poll delay: rows of one word per lane (<= 2048 cells) hand off sooner than a delay of 8 (~250 ns) waits;
-    // 2048^2 0.42 vs 0.44 us/generation, 2048 x 1024 0.40 vs 0.43, but 4096 x 2048 0.69 vs 0.65 and 4096^2 0.69 vs
-    // 0.68 (profiles/r4/coop_d_t.log); the rows-on-lanes pass keeps 8 (level at 4096^2, lanes_ab_h.log)
-    tune.poll_delay = b->opt.coop_poll_delay >= 0 ? b->opt.coop_poll_delay : (!lanes && W <= 2048 ? 0 : 8);
+    // first-poll delay (s_sleep periods): the cooperative pass polls at once up to 4096 cells per row (16-byte granules:
+    // 4096^2 0.557 at 0 vs 0.560 at 4, 2048^2 0.405 vs 0.413, 1024^2 0.458 vs 0.468 us/generation) and after 24 on
+    // 8192-wide rows, where a poll sent at once mostly misses (8192 x 4096 1.01 vs 1.12 at 16, 1.04 at 32; 8192 x 2048
+    // 0.88 vs 1.01) -- profiles/r5/ab_xcd_h.log; the rows-on-lanes pass keeps 8 (level at 4096^2, lanes_ab_h.log)
+    tune.poll_delay = b->opt.coop_poll_delay >= 0 ? b->opt.coop_poll_delay : (lanes ? 8 : (W <= 4096 ? 0 : 24));
     tune.spin_limit = (unsigned)std::min<int64_t>(b->opt.coop_spin_limit, 0xffffffffLL);
     tune.plain_launch = !b->opt.coop_launch;
     while (gens > 0) {
@@ -1424,7 +1428,10 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
     } else if (n == "coop_max_cells") o.coop_max_cells = value;
     else if (n == "resident_max_cells") o.resident_max_cells = value;
     else if (n == "wave_resident") o.wave_resident = value != 0;
-    else if (n == "split") {
+    else if (n == "split2") {
+        if (value < 0 || value >= 65536) return fail(GOL_ERR_INVALID, "split2 must be 0 (engine) .. 65535 (1/65536 units)");
+        o.split2 = (int32_t)value;
+    } else if (n == "split") {
         if (value >= 65536) return fail(GOL_ERR_INVALID, "split must be < 65536 (1/65536 units; 0 default, < 0 off)");
         o.split = (int32_t)(value < 0 ? -1 : value);
     } else if (n == "seg_rows") o.seg_rows = value < 0 ? 0 : value;
@@ -1522,6 +1529,7 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "resident_max_cells") *value = o.resident_max_cells;
     else if (n == "wave_resident") *value = o.wave_resident;
     else if (n == "split") *value = o.split;
+    else if (n == "split2") *value = o.split2;
     else if (n == "seg_rows") *value = o.seg_rows;
     else if (n == "seam") *value = o.seam;
     else if (n == "ragged_stream") *value = o.ragged_stream;

@@ -23,6 +23,9 @@ struct StreamArgs {
                         // 0 = one segment per wave)
     int32_t spare;      // waves to leave free for concurrent launches (plan_stream)
     int32_t split_opt;  // 0: the engine's pair split; > 0: this split (1/65536); < 0: none (board option "split")
+    int32_t split2;     // filled by plan_stream: three-wave groups, the middle wave's share of the middle + youngest
+                        // waves' rows (1/65536); 0 = the same ratio as the pair split (geometric shares)
+    int32_t split2_opt; // 0: the engine's; > 0: this value (board option "split2")
     int64_t seg_opt;    // 0: plan the segment length; > 0: rows per segment (board option "seg_rows")
     // Seam geometry (torus, filled by plan_stream; gol_step.hip): `nstrips` strips of 63 stored blocks plus one seam
     // lane holding both halos, and the rem = nblocks - 63 * nstrips blocks left over in remainder waves that pack
@@ -44,7 +47,8 @@ int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 // rag_bits: cells in the last word of a ragged row (words = ceil(W / 32), ilv 1), 0 for whole-word rows
 int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0);
-int stream_pair_split(int k, int ilv, bool bounded);
+int stream_pair_split(int k, int ilv, bool bounded, bool wrap);
+int stream_split2(int k, int ilv, bool bounded, bool wrap);
 int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits = 0);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless a.seg_opt -- the "seg_rows" option -- is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);

@@ -49,10 +49,10 @@ static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;
 // ONE workgroup fills a CU and the waves sharing a SIMD (w, w + 4, w + 8) belong to the same workgroup
 // (their age order is then known: see the group split in plan_stream).  (K, M) = (12, 2) runs 12-wave
 // workgroups at 3 waves/SIMD (168 VGPRs; profiles/r1/w12_sweep*.log) in both torus variants and on bounded
-// boards at least a strip wide (edge-fill strips: row masks only, 164 VGPRs).  The NARROW bounded variant (a
-// board narrower than one strip) also carries per-lane column masks, which spill at that budget (185 VGPRs;
-// round 1 measured 41k GCUPS with 12-wave workgroups, 74k with 8, profiles/r1/strip_bounded_sweep.log), so it
-// keeps 8.
+// boards at least a strip wide (edge-fill strips: row masks only, 153 VGPRs; ragged rows, NARROW = 2, the same with
+// their column-mask AND).  The NARROW = 1 bounded variant (a board narrower than one strip) also carries per-lane
+// column masks in its row-mask op, which spill at that budget (185 VGPRs; round 1 measured 41k GCUPS with 12-wave
+// workgroups, 74k with 8, profiles/r1/strip_bounded_sweep.log), so it keeps 8.
 template <int K, int M, bool BOUNDED, bool WRAP_ROWS, int NARROW>
 struct Wpb {
     static constexpr int value = NARROW != 1 && K == 12 && M == 2 ? 12 : kWavesPerBlock;
@@ -228,7 +228,8 @@ struct StreamWave {
     static constexpr int kStripBlocks = kNoHalo ? kWave : kInterior;
     // per-lane column masks: narrow (or ragged) bounded boards, and the K = 1 halo-free strips (their last strip
     // may end past the board's last block)
-    static constexpr bool kColMask = BOUNDED && (NARROW != 0 || kNoHalo);
+    // (NARROW = 2 keeps its column masks too, applied by their own AND: kRagEdge)
+    static constexpr bool kColMask = BOUNDED && (NARROW == 1 || kNoHalo);
 
     // Seam strips (torus deep passes, a.seam): lanes 0..62 hold 63 consecutive blocks and all store; lane 63, the
     // SEAM lane, holds the first half of the block right of lane 62 (bits 0..15 of its words: cells 0..16M-1 of
@@ -337,11 +338,15 @@ struct StreamWave {
         if (i >= n) return len;
         const float f = (float)a.split * (1.0f / 65536.0f);
         const float rho = (1.0f - f) / f;
+        // a.split2 (three-wave groups): the middle wave's share of the two younger waves' rows, so the ratio between
+        // the youngest and the middle wave is set apart from the one between the middle and the oldest
+        const float f2 = a.split2 > 0 ? (float)a.split2 * (1.0f / 65536.0f) : f;
+        const float rho2 = (1.0f - f2) / f2;
         float pw = 1.0f, sum = 0.0f, head = 0.0f;
         for (int j = 0; j < n; j++) {
             if (j == i) head = sum;
             sum += pw;
-            pw *= rho;
+            pw *= j == 0 ? rho : rho2;
         }
         const float total = (float)(len + 2 * K * n);
         int64_t cut = (int64_t)(total * head / sum + 0.5f) - 2 * K * i;
@@ -678,7 +683,7 @@ struct StreamWave {
                 else if constexpr (kSeam)
                     v[r][j] = lut3<0xD8>(0xffff0000u, t.s[kSeam ? r : 0][j], v[r][j]);
                 else if constexpr (BOUNDED)
-                    v[r][j] = kColMask ? lut3<0x80>(v[r][j], colmask[j], rm) : v[r][j] & rm;
+                    v[r][j] = kColMask || kRagEdge ? lut3<0x80>(v[r][j], colmask[j], rm) : v[r][j] & rm;
             }
         }
     }
@@ -704,7 +709,10 @@ struct StreamWave {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
             if (kRagged) out[j] &= rag_mask;
             if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask[j], rowmask) : out[j] & rowmask;  // dead off the board
-            if (kRagEdge && !MASK) out[j] &= colmask[j];  // a ragged row's cells past its end, at every level
+            // a ragged row's cells past its end, at every level: an AND of its own after the row mask (round 5: folded
+            // into the row mask's 3-input op, as for NARROW = 1, the (12, 2) pass needed 172 VGPRs and spilled 4 at its
+            // 168-VGPR budget; this form needs 153)
+            if (kRagEdge) out[j] &= colmask[j];
             sP[j] = sN[j];
             cP[j] = cN[j];
         }
@@ -1069,10 +1077,15 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
 // ------------------------------------------------------------------------------------------------
 // Supported (K, M) instantiations.  M = 1: any board with W % 32 == 0; M = 2 / 4 need W % 64 / 128.
 // Deeper K needs 5*M*K window registers per lane, so the deepest K shrinks as M grows.
+// (a register-usage study may compile a subset: -DGOL_KM_SUBSET(X)='X(12, 2)')
+#ifdef GOL_KM_SUBSET
+#define GOL_FOR_EACH_KM(X) GOL_KM_SUBSET(X)
+#else
 #define GOL_FOR_EACH_KM(X)                                                                               \
     X(1, 1) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(24, 1) X(32, 1)                                           \
     X(1, 2) X(2, 2) X(4, 2) X(8, 2) X(12, 2) X(16, 2)                                                    \
     X(1, 4) X(2, 4) X(4, 4) X(6, 4) X(8, 4)
+#endif
 
 bool stream_supported(int k, int ilv) {
 #define GOL_SUP(K_, M_) \
@@ -1157,8 +1170,15 @@ int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_b
 // equal segments it finishes early and leaves the younger alone at the single-wave issue rate
 // (tools/tail.py: 65536^2, K = 16 -- waves 0-3 of every workgroup busy 489 us, waves 4-7 747 us).
 // A board's "split" option (gol_set_option) overrides it for experiments.
-int stream_pair_split(int k, int ilv, bool bounded) {
+int stream_pair_split(int k, int ilv, bool bounded, bool wrap) {
     if (kWavesPerBlock < 8) return 0;
+    // Round 5, with the middle wave's share set apart (stream_split2), at the bench window (generation 300+), 4
+    // interleaved rounds (profiles/r5/split2_confirm_g.jsonl, us per pass, mean): single-board torus (12, 2) 0.66 / 0.76
+    // 442.5 against 0.70 / geometric 445.8; bounded (12, 2) 0.60 / 0.72 431.0 against 0.64 / geometric 436.0.  The
+    // per-role tails of a stamped build (profiles/r5/split2_tails_f.jsonl): torus roles ending at 439 / 378 / 436 us with
+    // geometric shares, 440 / 417 / 430 with 0.68 / 0.76.  (The ghost-row strips of N > 1 keep their measured split.)
+    if (bounded && ilv == 2 && k == 12) return (int)(0.60 * 65536);
+    if (!bounded && wrap && ilv == 2 && k == 12) return (int)(0.66 * 65536);
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
     // (12, 2) runs 12-wave workgroups at 3 waves/SIMD: three-way groups (profiles/r1/w12_sweep*.log)
@@ -1167,7 +1187,7 @@ int stream_pair_split(int k, int ilv, bool bounded) {
     // 107.6k / 104.7k; bounded (12, 2) 0.60 / 0.64 / 0.68 -> 96.6k / 99.0k / 95.4k; bounded (16, 2) 0.56 / 0.60 /
     // 0.64 / 0.68 -> 112.5k / 112.0k / 106.2k / 100.7k (a slope now, not round 2's cliff).
     if (bounded && ilv == 2 && k == 16) return (int)(0.60 * 65536);
-    if (bounded && ilv == 2 && k == 12) return (int)(0.64 * 65536);
+    // (bounded (12, 2): 0.64 until round 5, above)
     if (ilv == 1 && k >= 24) return (int)(0.60 * 65536);
     if (ilv == 2 && k == 12) return (int)(0.70 * 65536);
     if (ilv == 2 && k >= 16) return (int)(0.66 * 65536);
@@ -1218,8 +1238,16 @@ static bool seam_applies(const StreamArgs& a, int k, bool bounded) {
 // grid ONE balanced round of resident waves (a partial second round would leave a tail of lone waves), with
 // segments no shorter than 2K rows (pipeline fill cost).  a.split_opt / a.seg_opt / a.seam_opt (a board's "split" /
 // "seg_rows" / "seam" options) override the split, the segment length and the geometry for experiments.
+// Three-wave groups: the middle wave's share of the two younger waves' rows (1/65536), 0 = geometric.
+int stream_split2(int k, int ilv, bool bounded, bool wrap) {
+    if (kWavesPerBlock < 8 || ilv != 2 || k != 12) return 0;  // (12, 2): the one three-wave group variant
+    if (bounded) return (int)(0.72 * 65536);
+    return wrap ? (int)(0.76 * 65536) : 0;
+}
+
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
-    a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded));
+    a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded, wrap));
+    a.split2 = a.split2_opt > 0 ? a.split2_opt : stream_split2(k, a.ilv, bounded, wrap);
     const int64_t nblocks = a.words / a.ilv;
     a.seam = seam_applies(a, k, bounded) ? 1 : 0;
     a.rem = 0;

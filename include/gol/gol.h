@@ -173,6 +173,8 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *   "wave_resident" 1 | 0        single-wave pass for boards up to 128 x 256
  *   "split" 0 | n | -1           streaming pass: the oldest wave's share of a SIMD group segment in 1/65536
  *                                (0: the measured default, -1: no split)
+ *   "split2" 0 | n               streaming pass, three waves per SIMD group: the middle wave's share of the two
+ *                                younger waves' rows in 1/65536 (0: the measured default)
  *   "seg_rows" 0 | n             streaming pass: rows per wave segment (0: planned)
  *   "seam" 0 | -1                streaming pass on a torus: seam strips where they apply (-1: halo-lane strips)
  *   "transport" 1 | 2            multi-part boards: halo rows by peer copies (1) or RCCL (2, distinct devices;

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--boundary", type=int, default=0)
     p.add_argument("--ilv", type=int, default=0, help="packed layout (0 = the engine default for the width)")
     p.add_argument("--split", type=float, default=None, help="board option 'split' (fraction; negative = off)")
+    p.add_argument("--split2", type=float, default=None, help="board option 'split2' (fraction, three-wave groups)")
     p.add_argument("--seam", type=int, default=0, help="board option 'seam' (0 = engine choice, -1 = halo-lane strips)")
     p.add_argument("--pre", type=int, default=0, help="generations stepped before the timed passes (bench.py's window "
                    "starts at generation 312)")
@@ -34,6 +35,8 @@ def main():
     opts = {"coop": 0, "seam": a.seam}
     if a.split is not None:
         opts["split"] = int(a.split * 65536) if a.split >= 0 else -1
+    if a.split2 is not None:
+        opts["split2"] = int(a.split2 * 65536)
     for k in [int(x) for x in a.ks.split(",")]:
         if not lib.gol_supported_k(k, ilv):
             continue
@@ -44,7 +47,7 @@ def main():
             t = b.step_timed(a.passes * k) / 1e6 / a.passes
             h = b.hash()
             gcups = W * H * k / t / 1e9
-            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "split": a.split, "pre": a.pre, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
+            print(json.dumps({"W": W, "H": H, "ilv": ilv, "k": k, "seam": a.seam, "split": a.split, "split2": a.split2, "pre": a.pre, "us_per_pass": round(t * 1e6, 1), "gcups": round(gcups, 1),
                               "alg_GBps": round(W * H / 4 / t / 1e9, 1), "hash": f"{h:016x}",
                               }), flush=True)
 

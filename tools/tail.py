@@ -22,6 +22,8 @@ def main():
     p.add_argument("--k", type=int, default=16)
     p.add_argument("--boundary", type=int, default=0)
     p.add_argument("--pre", type=int, default=0, help="generations stepped before the stamped passes")
+    p.add_argument("--split", type=float, default=None, help="board option 'split' (fraction)")
+    p.add_argument("--split2", type=float, default=None, help="board option 'split2' (fraction)")
     a = p.parse_args()
     from gameoflifewithactors_amd import Board, _lib
 
@@ -29,7 +31,12 @@ def main():
     fn = lib.gol_debug_stamps
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_longlong]
     n = a.size
-    with Board(n, n, a.boundary, tblock_k=a.k) as b:
+    opts = {}
+    if a.split is not None:
+        opts["split"] = int(a.split * 65536)
+    if a.split2 is not None:
+        opts["split2"] = int(a.split2 * 65536)
+    with Board(n, n, a.boundary, tblock_k=a.k, options=opts) as b:
         b.seed_splitmix(1)
         if a.pre:
             b.step(a.pre)
@@ -44,7 +51,11 @@ def main():
             span = t1.max() - t0.min()
             busy = t1 - t0
             ends = t1 - t0.min()
-            print(json.dumps({"rep": rep, "waves": int(m.sum()), "span_us": round(span, 1),
+            wpb = 12 if a.k == 12 else 8
+            ids = np.nonzero(m)[0]
+            role_end = [round(float(np.median(ends[((ids % wpb) >> 2) == r])), 1) for r in range(wpb // 4)]
+            print(json.dumps({"rep": rep, "split": a.split, "split2": a.split2, "role_end_p50_us": role_end,
+                              "waves": int(m.sum()), "span_us": round(span, 1),
                               "busy_mean_us": round(busy.mean(), 1), "busy_min_us": round(busy.min(), 1),
                               "busy_max_us": round(busy.max(), 1),
                               "start_spread_us": round(t0.max() - t0.min(), 1),
