@@ -475,12 +475,15 @@ int coop_depth(const gol_board* b) {
 // The rows-on-lanes band pass (gol_lanes.hip) on a packed single board, for a call of `gens` generations: the boards
 // the cooperative pass would take whose width splits into windows (64 (m - 1) columns each), calls of at least two
 // hand-off blocks (the pass stages the board through LDS at both ends of a launch).
-// By default (option "lanes" 2) it takes the sizes where it measured faster than the cooperative pass
-// (profiles/r4/lanes_ab_j.log, us/generation, lanes vs cooperative): rows of <= 1024 cells (m = 5: 256^2 0.35 vs
-// 0.49, 512^2 0.37 vs 0.49, 1024 x 2048 0.41 vs 0.51) and 8192-wide boards up to 4096 rows (m = 9: 8192 x 2048 1.08
-// vs 1.55, 8192 x 4096 1.20 vs 1.63); the cooperative pass keeps 2048- and 4096-wide boards (4096^2 0.74 vs 0.69,
-// 2048 x 1024 0.50 vs 0.43) and taller 8192-wide ones (8192^2 3.1 vs 1.9).
-bool lanes_by_size(int64_t W, int64_t H) { return W <= 1024 || (W == 8192 && H <= 4096); }
+// By default (option "lanes" 2) it takes the sizes where it measured faster than the cooperative pass: rows of <= 1024
+// cells (profiles/r4/lanes_ab_j.log, us/generation, lanes vs cooperative: 256^2 0.35 vs 0.49, 512^2 0.37 vs 0.49, 1024 x
+// 2048 0.41 vs 0.51).  Round 4 also gave it 8192-wide boards up to 4096 rows (m = 9: 8192 x 2048 1.08 vs 1.55); round
+// 5's 16-byte granules took the cooperative pass there to 0.88-0.98 / 1.01-1.09 against 1.10 / 1.18 for the lanes
+// (profiles/r5/coop_delay_ab_m.log, coop_errword_ab_l.log), so 2048- to 8192-wide boards are the cooperative pass's.
+bool lanes_by_size(int64_t W, int64_t H) {
+    (void)H;
+    return W <= 1024;
+}
 // Its hand-off depth: the "coop_k" option if set, else up to 10 on rows of <= 1024 cells (the deepest a 32-row
 // window holds beside a band of >= k rows; there the pass is hand-off bound: 256^2 bounded 0.32 vs 0.36 us/generation
 // at k = 8, 512^2 0.33 vs 0.37, 1024 x 2048 0.36 vs 0.41, profiles/r4/lanes_k_o.log), else the cooperative depth.
@@ -559,11 +562,12 @@ int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w
     }
     gol::CoopTuning tune;
     tune.min_rows = b->opt.coop_r;
-    // first-poll delay (s_sleep periods): the cooperative pass polls at once up to 4096 cells per row (16-byte granules:
-    // 4096^2 0.557 at 0 vs 0.560 at 4, 2048^2 0.405 vs 0.413, 1024^2 0.458 vs 0.468 us/generation) and after 24 on
-    // 8192-wide rows, where a poll sent at once mostly misses (8192 x 4096 1.01 vs 1.12 at 16, 1.04 at 32; 8192 x 2048
-    // 0.88 vs 1.01) -- profiles/r5/ab_xcd_h.log; the rows-on-lanes pass keeps 8 (level at 4096^2, lanes_ab_h.log)
-    tune.poll_delay = b->opt.coop_poll_delay >= 0 ? b->opt.coop_poll_delay : (lanes ? 8 : (W <= 4096 ? 0 : 24));
+    // first-poll delay (s_sleep periods, 64 clocks each), measured after the error word left the hand-off's critical
+    // path (profiles/r5/coop_delay_ab_m.log, us/generation): 4096-wide rows poll at once (4096^2 0.535 at 0 / 0.537 at 4
+    // / 0.548 at 8), narrower rows after 4 (1024^2 0.447 against 0.453 at 0; 2048 x 1024 0.383 against 0.385; 2048^2
+    // 0.408 against 0.409), 8192-wide rows after 24 (8192 x 4096 1.09 against 1.11 at 40 and 1.16 at 64); the
+    // rows-on-lanes pass keeps 8 (256^2 bounded 0.253 against 0.253 at 0 and 0.268 at 16; lanes_small_m.log)
+    tune.poll_delay = b->opt.coop_poll_delay >= 0 ? b->opt.coop_poll_delay : (lanes ? 8 : (W < 4096 ? 4 : (W == 4096 ? 0 : 24)));
     tune.spin_limit = (unsigned)std::min<int64_t>(b->opt.coop_spin_limit, 0xffffffffLL);
     tune.plain_launch = !b->opt.coop_launch;
     while (gens > 0) {

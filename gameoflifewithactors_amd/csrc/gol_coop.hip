@@ -43,17 +43,12 @@ constexpr int kWaves = 16;                 // waves per workgroup: 4 per SIMD
 constexpr int kThreads = 64 * kWaves;
 constexpr int kMinLds = 96 * 1024;         // > half the CU's 160 KiB: one workgroup per CU
 constexpr unsigned kSpinLimit = 1u << 25;  // ~ 2 s: a wait this long means a band is not resident (default)
-// The wave-edge exchange per generation (GOL_COOP_XCH, A/B): 0 = the edge rows' horizontal sums (sum and carry of the
-// first and last row) in planes of one dword per lane, so no reader re-sums a neighbour's row; 1 = the same with a
-// lane's M words side by side (ds_write/read_b64 at M = 2: 8 of a wave's 2-cycle LDS reads per generation become 4);
-// 2 = the raw edge rows, lane-major, re-summed by the reader (half the LDS bytes, 16 more VALU slots per wave).
-// At 4096^2 the LDS carries 16 waves x (4 write2 + 4 read2) per generation, ~640 of its ~1300 cycles
-// (MI355X_MICROARCH.md "LDS": ds_write2_b32 6 cycles, ds_read2_b32 4).
-#ifndef GOL_COOP_XCH
-#define GOL_COOP_XCH 0
-#endif
-constexpr int kXch = GOL_COOP_XCH;
-constexpr int kSlotRows = kXch == 2 ? 2 : 4;  // LDS words per lane and word of a row, per wave and parity
+// The wave-edge exchange per generation carries the edge rows' horizontal sums (sum and carry of the first and last
+// row) in planes of one dword per lane, so no reader re-sums a neighbour's row.  Round 5 re-measured the
+// alternatives (profiles/r5/coop_xch_ab_k.log, 4096^2 torus, us/generation): the same sums lane-major with
+// ds_write/read_b64 0.571 against 0.558, the raw edge rows lane-major (half the LDS bytes, re-summed by the reader)
+// 0.638 -- the generation is bound by its VALU chain, not by the LDS (MI355X_MICROARCH.md "LDS").
+constexpr int kSlotRows = 4;  // LDS words per lane and word of a row, per wave and parity
 // LDS slots per parity: one per wave, plus a zero slot on each side (the neighbours of the first and last
 // waves), so every wave reads its neighbours' slots without a branch
 constexpr int kSlots = kWaves + 2;
@@ -109,20 +104,33 @@ __device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M],
 // short delay (`delay` s_sleep 1 periods, 8 by default: ~250 ns); 4096^2 0.70 vs 0.72 us/generation, bounded
 // 0.68 vs 0.74, 2048^2 0.41 vs 0.44 (profiles/r2/coop_delay_za.log).  Wider rows (M = 4: 8 granules per lane and
 // row pair) ran slower batched (8192 x 4096 1.69 vs 1.61) and poll granule by granule, at once.
+// Status of a hand-off wait: the granules arrived, the wait timed out, or another wave of the launch had timed out
+// (the launch's error word): the board is invalid, stop waiting.
+constexpr int kGot = 0, kTimedOut = 1, kLaunchFailed = 2;
+// The error word is read only by a wave that is still waiting, every 32 polls (round 5: read before every poll round,
+// its load was a memory round trip on the hand-off's critical path -- and its s_waitcnt also waited for the wave's
+// own write-through granule stores -- at every block).
+__device__ __forceinline__ bool launch_failed(const int* err) {
+    return __builtin_amdgcn_ballot_w64(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) != 0;
+}
 template <int M, int R>
-__device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uint32_t (&w)[R][M], unsigned tag,
-                                            int delay, unsigned spin_limit) {
+__device__ __forceinline__ int ld_granules(const uint64_t* const (&src)[R], uint32_t (&w)[R][M], unsigned tag,
+                                           int delay, unsigned spin_limit, const int* err) {
     if constexpr (M >= 4) {
-        bool ok = true;
+        int st = kGot;
 #pragma unroll
         for (int i = 0; i < R; i++) {
             if (!src[i]) continue;
 #pragma unroll
             for (int t = 0; t < M; t++) {
                 uint64_t g = __hip_atomic_load(src[i] + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (unsigned it = 0; ok && (unsigned)(g >> 32) != tag; it++) {  // after a timeout: no more waits
+                for (unsigned it = 0; st == kGot && (unsigned)(g >> 32) != tag; it++) {  // after a failure: no more waits
                     if (it == spin_limit) {
-                        ok = false;
+                        st = kTimedOut;
+                        break;
+                    }
+                    if ((it & 31) == 31 && launch_failed(err)) {
+                        st = kLaunchFailed;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
@@ -131,7 +139,7 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
                 w[i][t] = (uint32_t)g;
             }
         }
-        return ok;
+        return st;
     }
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
     uint64_t v[R][M];
@@ -148,7 +156,8 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
 #pragma unroll
             for (int t = 0; t < M; t++) miss = miss || (unsigned)(v[i][t] >> 32) != tag;
         if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
-        if (it == spin_limit) return false;
+        if (it == spin_limit) return kTimedOut;
+        if ((it & 31) == 31 && launch_failed(err)) return kLaunchFailed;
         __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
@@ -156,7 +165,7 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* const (&src)[R], uin
         if (src[i])
 #pragma unroll
             for (int t = 0; t < M; t++) w[i][t] = (uint32_t)v[i][t];
-    return true;
+    return kGot;
 }
 
 // 16-byte hand-off (round 5): a lane's granules in pairs, as 16-byte write-through stores and 16-byte sc1 polls
@@ -243,20 +252,43 @@ __device__ __forceinline__ void take16(const int (&off)[R], const typename Gran<
 #pragma unroll
             for (int t = 0; t < Gran<M>::N; t++) Gran<M>::take(v[i][t], &w[i][Gran<M>::G * t]);
 }
+#ifndef GOL_COOP_M4ERR
+#define GOL_COOP_M4ERR 0
+#endif
+// GOL_COOP_SENT (A/B): after a missed round, poll one granule pair per lane (its first needed row) until it carries the
+// tag, then the whole batch again -- a missed round of 8-wide rows is 4 KB per wave, 8 MB over the chip
+#ifndef GOL_COOP_SENT
+#define GOL_COOP_SENT 0
+#endif
 template <int M, int R>
-__device__ __forceinline__ bool ld_granules16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R], uint32_t (&w)[R][M],
-                                              unsigned tag, int delay, unsigned spin_limit) {
+__device__ __forceinline__ int ld_granules16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R], uint32_t (&w)[R][M],
+                                             unsigned tag, int delay, unsigned spin_limit, const int* err) {
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
     typename Gran<M>::V v[R][Gran<M>::N];
     issue16<M, R>(xrs, off, v);
+#if GOL_COOP_SENT
+    int first = kNoGranule;
+#pragma unroll
+    for (int i = R - 1; i >= 0; i--) first = off[i] != kNoGranule ? off[i] : first;
+#endif
     for (unsigned it = 0;; it++) {
         if (hit16<M, R>(off, v, tag)) break;
-        if (it == spin_limit) return false;
+        if (it == spin_limit) return kTimedOut;
+        if ((it & 31) == 31 && launch_failed(err)) return kLaunchFailed;
         __builtin_amdgcn_s_sleep(1);
+#if GOL_COOP_SENT
+        for (;; it++) {
+            const typename Gran<M>::V g = Gran<M>::load(xrs, first);
+            if (__builtin_amdgcn_ballot_w64(first != kNoGranule && Gran<M>::miss(g, tag)) == 0) break;
+            if (it == spin_limit) return kTimedOut;
+            if ((it & 31) == 31 && launch_failed(err)) return kLaunchFailed;
+            __builtin_amdgcn_s_sleep(1);
+        }
+#endif
         issue16<M, R>(xrs, off, v);
     }
     take16<M, R>(off, v, w);
-    return true;
+    return kGot;
 }
 
 // Word of the lane to the left / right.  FULL (all 64 lanes hold words): DPP rotate on a torus, DPP shift with
@@ -337,34 +369,11 @@ __device__ __forceinline__ void ragged_row_sum(const uint32_t (&r)[M], int lane,
     }
 }
 
-// Lane-major LDS exchange at M = 2 written out (kXch 1, 2): one ds_write_b64 / ds_read_b64 per row of sums or raw
-// row.  Left to the compiler, the pairs merge into ds_write2st64_b64 / ds_read2st64_b64, which take longer than the
-// two single accesses (MI355X_MICROARCH.md "LDS": ds_read2_b64 8 cycles against 2 x 2; ds_write2_b64 13 against 2 x 6).
-// The reads wait for themselves (the outputs of an asm statement are taken as ready when it ends); the writes are
-// waited for before the generation's barrier (lds_drain).
-[[maybe_unused]] __device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-template <int OFF>
-__device__ __forceinline__ void lds_put2(uint32_t addr, const uint32_t (&v)[2]) {
-    const u32x2c x = {v[0], v[1]};
-    asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(addr), "v"(x), "i"(OFF) : "memory");
-}
-template <int OFF0, int OFF1>
-__device__ __forceinline__ void lds_get2x2(uint32_t addr, uint32_t (&v0)[2], uint32_t (&v1)[2]) {
-    u32x2c x0, x1;
-    asm volatile("ds_read_b64 %0, %2 offset:%3\n\tds_read_b64 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(x0), "=&v"(x1) : "v"(addr), "i"(OFF0), "i"(OFF1) : "memory");
-    v0[0] = x0.x, v0[1] = x0.y, v1[0] = x1.x, v1[1] = x1.y;
-}
-[[maybe_unused]] __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 template <int M, int R, int LAY, bool BOUNDED, bool FULL>
 __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     constexpr bool ILV = LAY == kLayInterleaved;
     constexpr bool RAG = LAY == kLayRagged;
-    // [2 parity][kSlots][kSlotRows][M][64 lanes] (kXch 1, 2: [kSlotRows][64 lanes][M]); slots 0 and kSlots - 1 stay zero
-    extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
+    extern __shared__ uint32_t xs[];  // [2 parity][kSlots][kSlotRows][M][64 lanes]; slots 0 and kSlots - 1 stay zero
     const int band = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -447,37 +456,32 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             bool any = false;
 #pragma unroll
             for (int i = 0; i < R; i++) any = any || src[i] != nullptr;
-            // Once any wave of the launch has timed out (this one, or another band's: the error word, read by every
-            // lane and agreed by ballot, so it stays a vector load) the board is invalid: stop waiting, so a launch
-            // with a non-resident band ends after about one spin limit instead of one per block.  No early exit:
-            // every wave still meets the generation barriers.
-            // G16: only the waves that wait read it -- its load's wait (vmcnt counts stores) would hold a publishing
-            // wave at the top of every block until its own write-through granule stores had completed
-            if (!G16 || __builtin_amdgcn_ballot_w64(any) != 0)
-                if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
-                                                                              __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
-                    failed = true;
-            bool got;
-            if constexpr (G16) {
-                int off[R];
+            // Once any wave of the launch has timed out (this one, or another band's: the error word, which a waiting
+            // wave reads every 32 polls) the board is invalid: stop waiting, so a launch with a non-resident band ends
+            // after about one spin limit instead of one per block.  No early exit: every wave still meets the
+            // generation barriers.
+            int st = kGot;
+#if GOL_COOP_M4ERR
+            // (A/B) rows of 256 words: the error word read before the poll, as before round 5's change
+            if constexpr (M >= 4)
+                if (!failed && __builtin_amdgcn_ballot_w64(any) != 0 && launch_failed(a.err)) failed = true;
+#endif
+            if (!failed && __builtin_amdgcn_ballot_w64(any) != 0) {
+                if constexpr (G16) {
+                    int off[R];
 #pragma unroll
-                for (int i = 0; i < R; i++) off[i] = src[i] ? (int)((src[i] - a.xch) * 8) : kNoGranule;
-                got = true;
-                if (!failed && __builtin_amdgcn_ballot_w64(any) != 0) {
-                    got = ld_granules16<M, R>(xrs, off, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
+                    for (int i = 0; i < R; i++) off[i] = src[i] ? (int)((src[i] - a.xch) * 8) : kNoGranule;
+                    st = ld_granules16<M, R>(xrs, off, w, tag_of(blk - 1), a.poll_delay, a.spin_limit, a.err);
                     // the polled rounds have all returned (the tag checks waited for them); saying so here keeps the
                     // wait-count pass from assuming poll loads in flight at the granule stores and generation loop
                     // below, where a vmcnt(0) would also wait for this wave's write-through stores
                     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                } else {
+                    st = ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit, a.err);
                 }
-            } else {
-                got = failed || __builtin_amdgcn_ballot_w64(any) == 0 ||
-                      ld_granules<M, R>(src, w, tag_of(blk - 1), a.poll_delay, a.spin_limit);
             }
-            if (!got) {
-                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                failed = true;
-            }
+            if (st == kTimedOut) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st != kGot) failed = true;
         }
 #if GOL_COOP_STAMP
         coop_stamp(band, wv, blk, 1);
@@ -492,36 +496,14 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             const int par = gen & 1;      // alternates across blocks too: no barrier separates them
             // the slot of wave wv - 1 (slot index wv): this wave's reads and writes are all at positive constant
             // offsets from it (one address per generation; the ds instructions' immediate offsets do the rest)
-            uint32_t* nb = xs + ((par * kSlots + wv) * kSlotRows * M) * 64 + (kXch ? lane * M : lane);
-            auto SL = [&](int w_rel, int q, int t) -> uint32_t& {
-                return kXch ? nb[(w_rel * kSlotRows + q) * 64 * M + t] : nb[((w_rel * kSlotRows + q) * M + t) * 64];
-            };
-            // a lane's M words of one LDS row: one ds access (lane-major layouts) or M
+            uint32_t* nb = xs + ((par * kSlots + wv) * kSlotRows * M) * 64 + lane;
             auto put = [&](int w_rel, int q, const uint32_t (&v)[M]) {
-                if constexpr (kXch && M == 2) {
-                    *(u32x2c*)&SL(w_rel, q, 0) = u32x2c{v[0], v[1]};
-                } else if constexpr (kXch && M == 4) {
-                    *(u32x4c*)&SL(w_rel, q, 0) = u32x4c{v[0], v[1], v[2], v[3]};
-                } else {
 #pragma unroll
-                    for (int t = 0; t < M; t++) SL(w_rel, q, t) = v[t];
-                }
+                for (int t = 0; t < M; t++) nb[((w_rel * kSlotRows + q) * M + t) * 64] = v[t];
             };
             auto get = [&](int w_rel, int q, uint32_t (&v)[M]) {
-                if constexpr (kXch && M == 2) {
-                    const u32x2c x = *(const u32x2c*)&SL(w_rel, q, 0);
-                    v[0] = x.x;
-                    v[1] = x.y;
-                } else if constexpr (kXch && M == 4) {
-                    const u32x4c x = *(const u32x4c*)&SL(w_rel, q, 0);
-                    v[0] = x.x;
-                    v[1] = x.y;
-                    v[2] = x.z;
-                    v[3] = x.w;
-                } else {
 #pragma unroll
-                    for (int t = 0; t < M; t++) v[t] = SL(w_rel, q, t);
-                }
+                for (int t = 0; t < M; t++) v[t] = nb[((w_rel * kSlotRows + q) * M + t) * 64];
             };
             auto row_sums = [&](const uint32_t (&r)[M], uint32_t (&sv)[M], uint32_t (&cv)[M]) {
                 if constexpr (RAG)
@@ -535,42 +517,15 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             const bool active = j < j_act;
             const bool sums = j <= j_act;
             uint32_t so[R][M], co[R][M];
-            // byte offsets of LDS rows from nb (lane-major layouts: constant offsets of the asm accesses)
-            constexpr int kRowB = 64 * M * 4;
-            [[maybe_unused]] const uint32_t nba = lds_addr(nb);
-            constexpr bool kAsm = kXch && M == 2;
-            if constexpr (kXch == 2) {
-                // the raw edge rows, while a producing neighbour reads them (inactive waves too: their rows border
-                // active ones); the wave's own row sums only while it produces
-                if (sums) {
-                    if constexpr (kAsm) {
-                        lds_put2<(1 * kSlotRows + 0) * kRowB>(nba, w[0]);
-                        lds_put2<(1 * kSlotRows + 1) * kRowB>(nba, w[R - 1]);
-                    } else {
-                        put(1, 0, w[0]);
-                        put(1, 1, w[R - 1]);
-                    }
-                }
-                if (active) {
-#pragma unroll
-                    for (int i = 0; i < R; i++) row_sums(w[i], so[i], co[i]);
-                }
-            } else if (sums) {
+            if (sums) {
                 // the row sums of the first and last rows, while a producing neighbour reads them (inactive waves
-                // too: their rows border active ones), so no wave re-sums a neighbour's row
+                // too: their rows border active ones)
 #pragma unroll
                 for (int i = 0; i < R; i++) row_sums(w[i], so[i], co[i]);
-                if constexpr (kAsm) {
-                    lds_put2<(1 * kSlotRows + 0) * kRowB>(nba, so[0]);
-                    lds_put2<(1 * kSlotRows + 1) * kRowB>(nba, co[0]);
-                    lds_put2<(1 * kSlotRows + 2) * kRowB>(nba, so[R - 1]);
-                    lds_put2<(1 * kSlotRows + 3) * kRowB>(nba, co[R - 1]);
-                } else {
-                    put(1, 0, so[0]);
-                    put(1, 1, co[0]);
-                    put(1, 2, so[R - 1]);
-                    put(1, 3, co[R - 1]);
-                }
+                put(1, 0, so[0]);
+                put(1, 1, co[0]);
+                put(1, 2, so[R - 1]);
+                put(1, 3, co[R - 1]);
             }
             // the wave's interior rows need no neighbour: stepped while the edge rows travel through LDS
             if (active) {
@@ -585,29 +540,13 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
                     }
                 }
             }
-            if constexpr (kAsm) lds_drain();
             __syncthreads();
             if (!active) continue;
             uint32_t sa[M], ca[M], sb[M], cb[M];
-            if constexpr (kXch == 2) {
-                uint32_t above[M], below[M];
-                if constexpr (kAsm) {
-                    lds_get2x2<(0 * kSlotRows + 1) * kRowB, (2 * kSlotRows + 0) * kRowB>(nba, above, below);
-                } else {
-                    get(0, 1, above);
-                    get(2, 0, below);
-                }
-                row_sums(above, sa, ca);
-                row_sums(below, sb, cb);
-            } else if constexpr (kAsm) {
-                lds_get2x2<(0 * kSlotRows + 2) * kRowB, (0 * kSlotRows + 3) * kRowB>(nba, sa, ca);
-                lds_get2x2<(2 * kSlotRows + 0) * kRowB, (2 * kSlotRows + 1) * kRowB>(nba, sb, cb);
-            } else {
-                get(0, 2, sa);
-                get(0, 3, ca);
-                get(2, 0, sb);
-                get(2, 1, cb);
-            }
+            get(0, 2, sa);
+            get(0, 3, ca);
+            get(2, 0, sb);
+            get(2, 1, cb);
             constexpr int kEdgeRows = R > 1 ? 2 : 1;  // rows 0 and R - 1 (interior rows are done)
 #pragma unroll
             for (int e = 0; e < kEdgeRows; e++) {

@@ -149,9 +149,13 @@ __device__ __forceinline__ void st_granules(uint64_t* p, int stride, const uint3
 
 // The lane's M granules (src == nullptr: the lane needs none), in one batch of 8-byte sc1 loads per poll round after
 // `delay` s_sleep periods; false after the spin limit.
+// Returns kGot, kTimedOut, or kLaunchFailed: the launch's error word (another wave timed out), read only while this
+// wave waits, every 32 polls -- not at every block, where its load (and its s_waitcnt, which also waited for the
+// wave's own granule stores) was a memory round trip in front of every hand-off.
+constexpr int kGot = 0, kTimedOut = 1, kLaunchFailed = 2;
 template <int M>
-__device__ __forceinline__ bool ld_granules(const uint64_t* src, int stride, uint32_t (&w)[M], unsigned tag, int delay,
-                                            unsigned spin_limit) {
+__device__ __forceinline__ int ld_granules(const uint64_t* src, int stride, uint32_t (&w)[M], unsigned tag, int delay,
+                                           unsigned spin_limit, const int* err) {
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
     uint64_t v[M];
     for (unsigned it = 0;; it++) {
@@ -163,13 +167,16 @@ __device__ __forceinline__ bool ld_granules(const uint64_t* src, int stride, uin
             miss = miss || (unsigned)(v[t] >> 32) != tag;
         }
         if (__builtin_amdgcn_ballot_w64(miss) == 0) break;  // wave-uniform exit
-        if (it == spin_limit) return false;
+        if (it == spin_limit) return kTimedOut;
+        if ((it & 31) == 31 &&
+            __builtin_amdgcn_ballot_w64(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
+            return kLaunchFailed;
         __builtin_amdgcn_s_sleep(1);
     }
     if (src)
 #pragma unroll
         for (int t = 0; t < M; t++) w[t] = (uint32_t)v[t];
-    return true;
+    return kGot;
 }
 
 template <int M, int MB, bool BOUNDED>
@@ -245,13 +252,11 @@ __global__ __launch_bounds__(1024) void gol_lane_pass(LaneArgs a) {
             const uint64_t* src = nullptr;
             if (r < K && up >= 0) src = xrow(par, up, 1, r);
             else if (r >= K + B && r < L && dn >= 0) src = xrow(par, dn, 0, r - K - B);
-            if (!failed && __builtin_amdgcn_ballot_w64(__hip_atomic_load(a.err, __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT) != 0) != 0)
-                failed = true;
-            if (!failed && __builtin_amdgcn_ballot_w64(src != nullptr) != 0 &&
-                !ld_granules<M>(src, 2 * K, w, tag_of(blk - 1), a.poll_delay, a.spin_limit)) {
-                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                failed = true;
+            // after a failed wait (this wave's, or another's: the error word, read while waiting) no more waits
+            if (!failed && __builtin_amdgcn_ballot_w64(src != nullptr) != 0) {
+                const int st = ld_granules<M>(src, 2 * K, w, tag_of(blk - 1), a.poll_delay, a.spin_limit, a.err);
+                if (st == kTimedOut) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (st != kGot) failed = true;
             }
         }
         for (int j = 0; j < k; j++) {

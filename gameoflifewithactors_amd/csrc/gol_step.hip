@@ -64,14 +64,22 @@ struct Wpb {
 // ROT (torus): rotates, so lane 0's left neighbour is lane 63 -- the seam lane of a seam strip, a halo lane (whose
 // outer edge is garbage anyway) otherwise.  Bounded boards shift with zero fill: the dead cells beyond the
 // board's edge in the edge-fill strips.
+// GOL_AB_TORUS_SHIFT, GOL_AB_NOSEAMDMA (timing studies only, WRONG boards): the torus deep pass with the bounded
+// pass's zero-fill shifts instead of rotates / without its seam DMA and merge, to price each against the bounded pass
+#ifndef GOL_AB_TORUS_SHIFT
+#define GOL_AB_TORUS_SHIFT 0
+#endif
+#ifndef GOL_AB_NOSEAMDMA
+#define GOL_AB_NOSEAMDMA 0
+#endif
 template <bool ROT>
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i-1
-    if (ROT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
+    if (ROT && !GOL_AB_TORUS_SHIFT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);              // wave_shr:1
 }
 template <bool ROT>
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i+1
-    if (ROT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
+    if (ROT && !GOL_AB_TORUS_SHIFT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);              // wave_shl:1
 }
 
@@ -328,6 +336,8 @@ struct StreamWave {
     // kRagged: west carry shift (32 - rag_bits on the lane holding word 0), east carry position (rag_bits - 1 on
     // the lane holding the last word, else 31) and the cells of the lane's word on the row
     uint32_t rag_shw = 0, rag_she = 31, rag_mask = 0xffffffffu;
+    // kRagEdge: this wave holds the ragged row's partial block (wave-uniform)
+    bool rag_wave = false;
 
     // First row (relative to the group segment of `len` rows) of the i-th oldest wave's share.  Shares
     // fall geometrically with age, ratio rho = (1 - f) / f (f = a.split / 65536 = the oldest wave's share
@@ -389,6 +399,12 @@ struct StreamWave {
             const bool in = cb >= 0 && cb < nblocks;
 #pragma unroll
             for (int j = 0; j < M; j++) colmask[j] = cell_mask(cb, j, nblocks);
+            if constexpr (kRagEdge) {
+                bool part = false;
+#pragma unroll
+                for (int j = 0; j < M; j++) part = part || colmask[j] != 0xffffffffu;
+                rag_wave = __builtin_amdgcn_ballot_w64(part) != 0;
+            }
             lc = in ? cb : 0;
         } else if (kRagged) {
             // strips of 62 stored words over the ring positions -o .. nw - 1 - o (o = a.rag_origin: 1, or 2 when
@@ -614,7 +630,7 @@ struct StreamWave {
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
                 rs = src_rs(src + br * a.pitch, span_bytes, 8);
-                if constexpr (kSeam1)
+                if constexpr (kSeam1 && !GOL_AB_NOSEAMDMA)
                     if (r == 0) stage_load_seam1<PAR>(br);
             }
             if constexpr ((KINDS & 2) == 0 && !kSeam1) row_rs[r] = rs;
@@ -655,7 +671,8 @@ struct StreamWave {
     }
     template <int PAR>
     __device__ __forceinline__ void stage_read_seam(Seam& t, int lane) {
-        if constexpr (kSeam1) {  // the same R x M words for every lane (a broadcast read)
+        if constexpr (kSeam1 && GOL_AB_NOSEAMDMA) {
+        } else if constexpr (kSeam1) {  // the same R x M words for every lane (a broadcast read)
 #pragma unroll
             for (int r = 0; r < R; r++)
 #pragma unroll
@@ -678,7 +695,9 @@ struct StreamWave {
             if constexpr (BOUNDED) rm = row_mask((int)first_step + r);
 #pragma unroll
             for (int j = 0; j < M; j++) {
-                if constexpr (kSeam1)
+                if constexpr (kSeam1 && GOL_AB_NOSEAMDMA)
+                    ;
+                else if constexpr (kSeam1)
                     v[r][j] = lut3<0xD8>(hmask, t.s[kSeam ? r : 0][j], v[r][j]);
                 else if constexpr (kSeam)
                     v[r][j] = lut3<0xD8>(0xffff0000u, t.s[kSeam ? r : 0][j], v[r][j]);
@@ -709,10 +728,6 @@ struct StreamWave {
             out[j] = life_next(sP[j], cP[j], sC[j], cC[j], sN[j], cN[j], alC[j]);
             if (kRagged) out[j] &= rag_mask;
             if (BOUNDED && MASK) out[j] = kColMask ? lut3<0x80>(out[j], colmask[j], rowmask) : out[j] & rowmask;  // dead off the board
-            // a ragged row's cells past its end, at every level: an AND of its own after the row mask (round 5: folded
-            // into the row mask's 3-input op, as for NARROW = 1, the (12, 2) pass needed 172 VGPRs and spilled 4 at its
-            // 168-VGPR budget; this form needs 153)
-            if (kRagEdge) out[j] &= colmask[j];
             sP[j] = sN[j];
             cP[j] = cN[j];
         }
@@ -781,6 +796,22 @@ struct StreamWave {
                     right[r] = from_right<!BOUNDED>(o0[0]);
                     right[r + 1] = from_right<!BOUNDED>(o1[0]);
                     __builtin_amdgcn_sched_barrier(kAllButDs);
+                }
+            }
+            if constexpr (kRagEdge) {
+                // a ragged row's cells past its end, dead at every level: only the wave holding the partial block
+                // masks (one uniform branch per level; the other waves run the NARROW = 0 arithmetic).  After the
+                // level, before the next one reads its rows: within a level only its inputs are read, and the
+                // neighbour words already sent on (`right`) carry the partial block's cell 0, which is on the board.
+                // (Round 4 ANDed every word of every wave at every level, in the row mask's 3-input op: the
+                // (12, 2) pass needed 172 VGPRs and spilled 4 at its 168-VGPR budget.)
+                // (in place, written out: a C++ AND made the compiler move the rows between registers on the
+                // other path to join the two)
+                if (rag_wave) {
+#pragma unroll
+                    for (int r = 0; r < R; r++)
+#pragma unroll
+                        for (int j = 0; j < M; j++) asm volatile("v_and_b32 %0, %0, %1" : "+v"(v[r][j]) : "v"(colmask[j]));
                 }
             }
             __builtin_amdgcn_sched_barrier(0);  // level g+1 may not be hoisted next to its exchanges

@@ -185,12 +185,12 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *                                never (0: ilv-1 rows)
  *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
  *                                words (0: the per-generation byte step)
- *   "coop_poll_delay" -1 | 0..4096  s_sleep periods before a hand-off's first poll (-1: 0 on cooperative-pass rows of
- *                                <= 2048 cells, else 8)
+ *   "coop_poll_delay" -1 | 0..4096  s_sleep periods before a hand-off's first poll (-1: on the cooperative pass 0 for
+ *                                4096-cell rows, 4 for narrower ones, 24 for 8192; 8 on the rows-on-lanes pass)
  *   "lanes" 2 | 1 | 0            rows-on-lanes band pass in place of the cooperative one (packed single boards whose
  *                                width splits into 128/256/512/1024-column windows, coop_k <= 10, calls of >= 2 k
  *                                generations, every band resident at once): 2 = on the sizes it
- *                                measured faster (rows of <= 1024 cells; 8192 wide up to 4096 rows), 1 = wherever it
+ *                                measured faster (rows of <= 1024 cells), 1 = wherever it
  *                                applies, 0 = never
  *   "lanes_m" 0 | 3 | 5 | 9 | 17 its words per lane and half-row (0: 3 up to 1024 columns, else 9 when W % 512 == 0)
  * Unknown names and out-of-range values return GOL_ERR_INVALID.  Results are bit-identical for every setting.
