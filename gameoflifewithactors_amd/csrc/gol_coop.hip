@@ -107,9 +107,10 @@ __device__ __forceinline__ void st_granules(uint64_t* p, const uint32_t (&w)[M],
 // Status of a hand-off wait: the granules arrived, the wait timed out, or another wave of the launch had timed out
 // (the launch's error word): the board is invalid, stop waiting.
 constexpr int kGot = 0, kTimedOut = 1, kLaunchFailed = 2;
-// The error word is read only by a wave that is still waiting, every 32 polls (round 5: read before every poll round,
-// its load was a memory round trip on the hand-off's critical path -- and its s_waitcnt also waited for the wave's
-// own write-through granule stores -- at every block).
+// The error word is read by a wave that is still waiting, every 32 polls (round 5: read before every poll round, its
+// load was a memory round trip on the hand-off's critical path -- and its s_waitcnt also waited for the wave's own
+// write-through granule stores -- at every block: 4096^2 0.554 -> 0.536 us/generation; rows of 256 words keep the
+// read in front of the poll, see the poll site).
 __device__ __forceinline__ bool launch_failed(const int* err) {
     return __builtin_amdgcn_ballot_w64(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) != 0;
 }
@@ -252,39 +253,17 @@ __device__ __forceinline__ void take16(const int (&off)[R], const typename Gran<
 #pragma unroll
             for (int t = 0; t < Gran<M>::N; t++) Gran<M>::take(v[i][t], &w[i][Gran<M>::G * t]);
 }
-#ifndef GOL_COOP_M4ERR
-#define GOL_COOP_M4ERR 0
-#endif
-// GOL_COOP_SENT (A/B): after a missed round, poll one granule pair per lane (its first needed row) until it carries the
-// tag, then the whole batch again -- a missed round of 8-wide rows is 4 KB per wave, 8 MB over the chip
-#ifndef GOL_COOP_SENT
-#define GOL_COOP_SENT 0
-#endif
 template <int M, int R>
 __device__ __forceinline__ int ld_granules16(__amdgpu_buffer_rsrc_t xrs, const int (&off)[R], uint32_t (&w)[R][M],
                                              unsigned tag, int delay, unsigned spin_limit, const int* err) {
     for (int i = 0; i < delay; i++) __builtin_amdgcn_s_sleep(1);
     typename Gran<M>::V v[R][Gran<M>::N];
     issue16<M, R>(xrs, off, v);
-#if GOL_COOP_SENT
-    int first = kNoGranule;
-#pragma unroll
-    for (int i = R - 1; i >= 0; i--) first = off[i] != kNoGranule ? off[i] : first;
-#endif
     for (unsigned it = 0;; it++) {
         if (hit16<M, R>(off, v, tag)) break;
         if (it == spin_limit) return kTimedOut;
         if ((it & 31) == 31 && launch_failed(err)) return kLaunchFailed;
         __builtin_amdgcn_s_sleep(1);
-#if GOL_COOP_SENT
-        for (;; it++) {
-            const typename Gran<M>::V g = Gran<M>::load(xrs, first);
-            if (__builtin_amdgcn_ballot_w64(first != kNoGranule && Gran<M>::miss(g, tag)) == 0) break;
-            if (it == spin_limit) return kTimedOut;
-            if ((it & 31) == 31 && launch_failed(err)) return kLaunchFailed;
-            __builtin_amdgcn_s_sleep(1);
-        }
-#endif
         issue16<M, R>(xrs, off, v);
     }
     take16<M, R>(off, v, w);
@@ -461,11 +440,13 @@ __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
             // after about one spin limit instead of one per block.  No early exit: every wave still meets the
             // generation barriers.
             int st = kGot;
-#if GOL_COOP_M4ERR
-            // (A/B) rows of 256 words: the error word read before the poll, as before round 5's change
+            // Rows of 256 words (M = 4) keep a read of the error word in front of their poll: there that memory round
+            // trip is worth its latency -- 8192 x 2048 0.89 against 0.99 us/generation without it, 8192 x 4096 1.03
+            // against 1.08, where no first-poll delay matched it (24 / 40 / 64: 0.98 / 1.00 / 1.06,
+            // profiles/r5/coop_poll_throttle_ab_n.log, coop_delay_ab_m.log).  A missed poll round of these rows is 4 KB
+            // per wave; polling one granule pair per lane after a miss was slower still (1.02).
             if constexpr (M >= 4)
                 if (!failed && __builtin_amdgcn_ballot_w64(any) != 0 && launch_failed(a.err)) failed = true;
-#endif
             if (!failed && __builtin_amdgcn_ballot_w64(any) != 0) {
                 if constexpr (G16) {
                     int off[R];
