@@ -72,6 +72,11 @@ struct Wpb {
 #ifndef GOL_AB_NOSEAMDMA
 #define GOL_AB_NOSEAMDMA 0
 #endif
+// GOL_AB_WRAPPTR (A/B): the single-board torus walks its rows with a running address (reset at the wrap), as the
+// bounded pass does, instead of a 64-bit row multiply per row
+#ifndef GOL_AB_WRAPPTR
+#define GOL_AB_WRAPPTR 0
+#endif
 template <bool ROT>
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i-1
     if (ROT && !GOL_AB_TORUS_SHIFT) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
@@ -518,7 +523,8 @@ struct StreamWave {
         }
         if constexpr (kStage) {
             const uint64_t pitch_bytes = (uint64_t)a.pitch * 4;
-            if (BOUNDED) lptr = (uint64_t)(uintptr_t)src + (uint64_t)load_br * pitch_bytes;  // (may precede the buffer)
+            if (BOUNDED || (GOL_AB_WRAPPTR && WRAP_ROWS))
+                lptr = (uint64_t)(uintptr_t)src + (uint64_t)load_br * pitch_bytes;  // (bounded: may precede the buffer)
             sd = -R - 2 * K;  // the first store (at trip 0's top) is trip -1's: nothing valid
             sptr = (uint64_t)(uintptr_t)dst + (uint64_t)((WRAP_ROWS ? 0 : a.ghost) + seg_begin + sd) * pitch_bytes;
         }
@@ -622,14 +628,16 @@ struct StreamWave {
                 lrow++;
             } else {
                 int64_t br = load_br;
+                [[maybe_unused]] const uint64_t p = lptr;
                 if (WRAP_ROWS) {
                     load_br = br + 1 == a.rows ? 0 : br + 1;
+                    if constexpr (GOL_AB_WRAPPTR) lptr = load_br == 0 ? (uint64_t)(uintptr_t)src : p + (uint64_t)a.pitch * 4;
                 } else {
                     const int64_t buf_rows = a.rows + 2 * a.ghost;
                     load_br = br + 1;
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
-                rs = src_rs(src + br * a.pitch, span_bytes, 8);
+                rs = src_rs(GOL_AB_WRAPPTR && WRAP_ROWS ? reinterpret_cast<const uint32_t*>(p) : src + br * a.pitch, span_bytes, 8);
                 if constexpr (kSeam1 && !GOL_AB_NOSEAMDMA)
                     if (r == 0) stage_load_seam1<PAR>(br);
             }
