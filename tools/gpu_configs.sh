@@ -1,7 +1,7 @@
 # GPU call script (gpurun): every BASELINE config on the round's final build (one line each; self-checked).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4c; mkdir -p $O
+O=gpurun_out/${CFG_TAG:-r4c}; mkdir -p $O
 step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   timeout -k 10 $secs "$@" > $O/$name.log 2>&1; local rc=$?
