@@ -1604,8 +1604,8 @@ int gol_strip_plan_ex(const gol_strip* s, int k, int64_t out_begin, int64_t out_
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a = strip_args(s, out_begin, out_end, 0, 0, 0);
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
-    const int64_t v[8] = {a.nstrips, a.nsegs, a.seg, a.seam, a.rem, a.rem_p, a.rem_mid, a.rem_units};
-    for (int i = 0; i < 8; i++) plan[i] = v[i];
+    const int64_t v[10] = {a.nstrips, a.nsegs, a.seg, a.seam, a.rem, a.rem_p, a.rem_mid, a.rem_units, a.split, a.split2};
+    for (int i = 0; i < (n < 10 ? 8 : 10); i++) plan[i] = v[i];
     return GOL_OK;
 }
 

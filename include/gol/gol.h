@@ -259,7 +259,8 @@ int gol_strip_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end
                    int64_t* seg_rows);
 /* The whole plan (n >= 8): plan[0..7] = column strips, row segments, rows per segment, seam geometry (1 / 0),
  * remainder blocks per row, remainder sub-strips per wave, packed remainder segments (segments 1 .. plan[6] share
- * remainder waves), remainder units.  Planned for the current device's resident waves (4096 without a device):
+ * remainder waves), remainder units; with n >= 10 also plan[8..9] = the SIMD groups' split and second split (1/65536
+ * units, 0 = unsplit / geometric).  Planned for the current device's resident waves (4096 without a device):
  * tests/test_cpu_host.py walks it to check that no wave reads outside its buffer. */
 int gol_strip_plan_ex(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* plan, int64_t n);
 

@@ -260,3 +260,24 @@ def test_seam_remainder_waves_stay_inside_the_buffer(words, ilv, k):
                     continue
                 for r, sy, j, row, buf_rows in _walk_rows(plan, k, rows, ghost, wrap, b, e):
                     assert 0 <= row < buf_rows, (rows, wrap, (b, e), plan, r, sy, j, row)
+
+
+@pytest.mark.parametrize("wrap,boundary,want", [(True, 0, (0.66, 0.76)), (False, 1, (0.60, 0.72)), (False, 0, (0.70, 0.0))])
+def test_stream_plan_group_split_defaults(wrap, boundary, want):
+    """Round 5: the (12, 2) deep pass's three-wave SIMD groups split a segment by two ratios (split, split2), tuned
+    per variant at the bench window (profiles/r5/split2_confirm_g.jsonl): single-board torus 0.66 /
+    0.76, bounded 0.60 / 0.72; ghost-row torus strips keep round 4's single ratio 0.70 (split2 0: geometric)."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    rows, k, words = 65536, 12, 2048
+    ghost = 0 if wrap else k
+    strip = _lib.Strip(words * 32, rows if wrap else rows * 2, 0, rows, ghost, words, boundary, 1 if wrap else 0, 2, 0)
+    plan = (ctypes.c_int64 * 10)()
+    assert lib.gol_strip_plan_ex(ctypes.byref(strip), k, 0, rows, plan, 10) == 0, lib.gol_last_error()
+    assert plan[8] == int(want[0] * 65536) and plan[9] == int(want[1] * 65536), list(plan)
+    plan8 = (ctypes.c_int64 * 8)()  # the 8-entry form still works and writes 8 entries
+    assert lib.gol_strip_plan_ex(ctypes.byref(strip), k, 0, rows, plan8, 8) == 0
+    assert list(plan8) == list(plan)[:8]
