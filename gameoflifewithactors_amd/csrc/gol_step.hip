@@ -72,6 +72,10 @@ struct Wpb {
 #ifndef GOL_AB_NOSEAMDMA
 #define GOL_AB_NOSEAMDMA 0
 #endif
+// GOL_AB_BSPREAD (A/B): the bounded deep passes spread their row DMAs over the levels as the torus ones do
+#ifndef GOL_AB_BSPREAD
+#define GOL_AB_BSPREAD 0
+#endif
 // GOL_AB_WRAPPTR (A/B): the single-board torus walks its rows with a running address (reset at the wrap), as the
 // bounded pass does, instead of a 64-bit row multiply per row
 #ifndef GOL_AB_WRAPPTR
@@ -954,7 +958,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             // prefetch placement (GOL_SEAM_SPREAD above): rows issued at the top, after level g, and after the levels
             // (the pipeline-fill trips, which skip levels, keep every DMA at the top)
             constexpr int kSpread = GOL_SEAM_SPREAD >= 0 ? GOL_SEAM_SPREAD : 4;
-            constexpr int kMode = W::kSeam && !decltype(skip)::value ? kSpread : 0;
+            constexpr int kMode = (W::kSeam || (BOUNDED && GOL_AB_BSPREAD)) && !decltype(skip)::value ? kSpread : 0;
             if constexpr (kMode == 0) w.template stage_load<1 - PAR>();
             if constexpr (kMode == 3) {
 #pragma unroll
