@@ -2,7 +2,7 @@
 # bounded), the config-2 command (torus, bounded).  Results under gpurun_out/r5final/.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r5final; mkdir -p $O
+O=gpurun_out/${GATE_TAG:-r5final}; mkdir -p $O
 step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
   timeout -k 10 $secs "$@" > $O/$name.log 2>&1; local rc=$?
