@@ -143,13 +143,15 @@ def test_debug_knobs_are_not_board_options(gol):
             assert lib.gol_debug_set_option(b._h, name.encode(), 0) == _lib.GOL_ERR_INVALID, name
 
 
-def test_coop_timeout_reported_on_every_readback(gol, oracle):
+@pytest.mark.parametrize("w,h", [(2048, 2048), (4096, 1024), (8192, 512)])
+def test_coop_timeout_reported_on_every_readback(gol, oracle, w, h):
     """A band hand-off wait that times out (forced here: a spin limit of one poll, while the neighbour band has not
     published yet) leaves a wrong board.  Every readback and gol_synchronize must report it (GOL_ERR_HIP), the
     launch must still end (no further waits once one has failed), and the board must be usable again once it is
-    overwritten."""
-    b0 = _rand(2048, 2048, 91)
-    with gol.Board(2048, 2048, 0, options={"coop": 1, "lanes": 0, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
+    overwritten.  Round 5: on each hand-off form -- 8-byte granules (M = 1), 16-byte pairs (M = 2),
+    and the 256-word rows that read the error word before polling (M = 4)."""
+    b0 = _rand(h, w, 91)
+    with gol.Board(w, h, 0, options={"coop": 1, "lanes": 0, "coop_k": 1, "coop_spin_limit": 1, "coop_poll_delay": 0}) as b:
         b.set_cells(b0)
         failed = False
         for _ in range(20):  # the race is lost almost always at once; a few tries make it certain
