@@ -72,6 +72,15 @@ struct Wpb {
 #ifndef GOL_AB_NOSEAMDMA
 #define GOL_AB_NOSEAMDMA 0
 #endif
+// GOL_SEAM_SMEM (round 5, default 1): the seam lane's half-blocks read by the scalar unit -- the R x M seam words of a
+// trip are the same for every lane, so each row's M words come as one s_load into SGPRs with the row's DMAs -- instead
+// of round 4's seam LDS-DMA and its broadcast LDS reads at the trip's top.  The (12, 2) torus pass drops from 164 to
+// 154 VGPRs; 4 interleaved rounds at the bench window (profiles/r5/torus_seam_smem_y.jsonl), us per pass: (12, 2)
+// 431.8 against 434.6, (16, 2) 603.6 against 608.3.  (The board buffer a pass reads is never written during it: the
+// scalar cache, refilled at every dispatch, holds no stale line.)
+#ifndef GOL_SEAM_SMEM
+#define GOL_SEAM_SMEM 1
+#endif
 // GOL_AB_BSPREAD (A/B): the bounded deep passes spread their row DMAs over the levels as the torus ones do
 #ifndef GOL_AB_BSPREAD
 #define GOL_AB_BSPREAD 0
@@ -299,6 +308,16 @@ struct StreamWave {
     // waves and halo-lane strips merge nothing)
     using SeamStage = uint32_t[2][kWave];
     SeamStage* seam1 = nullptr;
+    // GOL_SEAM_SMEM: the next trip's seam words (SGPRs), the seam column's byte offset in a row, and whether this wave
+    // merges a seam (a seam strip, not a remainder wave)
+    static constexpr bool kSmem = kSeam1 && GOL_SEAM_SMEM;
+    struct SmemSeam {
+        uint32_t s[R][M];
+        int64_t col;  // in words
+        bool on;
+    };
+    struct NoSmem {};
+    [[no_unique_address]] typename std::conditional<kSmem, SmemSeam, NoSmem>::type sm;
     int seam1_delta = 0;  // (lane / M) % R rows + the word (lane % M) of the block left of lane 0, in bytes
     uint32_t hmask = 0;
     template <int WORDS>
@@ -480,6 +499,14 @@ struct StreamWave {
                 seam1_delta = (int)(((lane / M) % R) * a.pitch * 4) + 4 * (lane % M) +
                               (a.seam && rem_count == 0 ? (int)(floor_mod(sx * kSeamInterior - 1, nblocks) * 4 * M) : 0);
                 hmask = a.seam && rem_count == 0 && lane == kWave - 1 ? 0xffff0000u : 0u;
+                if constexpr (kSmem) {
+                    sm.on = a.seam && rem_count == 0;
+                    sm.col = sm.on ? floor_mod(sx * kSeamInterior - 1, nblocks) * M : 0;
+#pragma unroll
+                    for (int r = 0; r < R; r++)
+#pragma unroll
+                        for (int j = 0; j < M; j++) sm.s[r][j] = 0u;
+                }
             }
         }
         seg_begin = a.out_begin + sy * a.seg;
@@ -642,8 +669,17 @@ struct StreamWave {
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
                 rs = src_rs(GOL_AB_WRAPPTR && WRAP_ROWS ? reinterpret_cast<const uint32_t*>(p) : src + br * a.pitch, span_bytes, 8);
-                if constexpr (kSeam1 && !GOL_AB_NOSEAMDMA)
+                if constexpr (kSmem) {
+                    if (sm.on) {  // wave-uniform: one scalar load of the row's M seam words
+                        typedef uint32_t su32xM __attribute__((ext_vector_type(M)));
+                        const auto* q = (const __attribute__((address_space(4))) su32xM*)(uintptr_t)(src + br * a.pitch + sm.col);
+                        const su32xM x = *q;
+#pragma unroll
+                        for (int j = 0; j < M; j++) sm.s[r][j] = x[j];
+                    }
+                } else if constexpr (kSeam1 && !GOL_AB_NOSEAMDMA) {
                     if (r == 0) stage_load_seam1<PAR>(br);
+                }
             }
             if constexpr ((KINDS & 2) == 0 && !kSeam1) row_rs[r] = rs;
 #pragma unroll
@@ -684,6 +720,11 @@ struct StreamWave {
     template <int PAR>
     __device__ __forceinline__ void stage_read_seam(Seam& t, int lane) {
         if constexpr (kSeam1 && GOL_AB_NOSEAMDMA) {
+        } else if constexpr (kSmem) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int j = 0; j < M; j++) t.s[r][j] = sm.s[r][j];
         } else if constexpr (kSeam1) {  // the same R x M words for every lane (a broadcast read)
 #pragma unroll
             for (int r = 0; r < R; r++)
@@ -954,6 +995,9 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             w.store_staged(B);
             w.template stage_read<PAR>(B, lane);
+            // (GOL_SEAM_SMEM: the seam words taken before this trip's prefetch loads the next trip's over them)
+            [[maybe_unused]] typename W::Seam st_smem;
+            if constexpr (W::kSmem) w.template stage_read_seam<PAR>(st_smem, lane);
             __builtin_amdgcn_sched_barrier(0);  // the row reads before the prefetch: their latency hides behind it
             // prefetch placement (GOL_SEAM_SPREAD above): rows issued at the top, after level g, and after the levels
             // (the pipeline-fill trips, which skip levels, keep every DMA at the top)
@@ -965,7 +1009,10 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
                 for (int r = 0; r < R; r++) w.template stage_load_row<1 - PAR, 1>(r);
             }
             typename W::Seam st;
-            w.template stage_read_seam<PAR>(st, lane);
+            if constexpr (W::kSmem)
+                st = st_smem;
+            else
+                w.template stage_read_seam<PAR>(st, lane);
             w.stage_in(B, st, tt * R);
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetch at the top of the trip
             auto hook = [&](int g) {
