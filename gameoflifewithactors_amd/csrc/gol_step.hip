@@ -315,6 +315,7 @@ struct StreamWave {
         uint32_t s[R][M];
         int64_t col;  // in words
         bool on;
+        int64_t row[R];  // GOL_SEAM_SMEM 2: the buffer rows of the next trip, loaded at the trip's end
     };
     struct NoSmem {};
     [[no_unique_address]] typename std::conditional<kSmem, SmemSeam, NoSmem>::type sm;
@@ -644,6 +645,25 @@ struct StreamWave {
             dma<1>(src_rs(base, left < R * pb ? left : R * pb, 6), lds, seam1_delta);
         }
     }
+    // GOL_SEAM_SMEM: one scalar load of row r's M seam words (wave-uniform address)
+    __device__ __forceinline__ void smem_seam_row(int r, int64_t br) {
+        if constexpr (kSmem) {
+            typedef uint32_t su32xM __attribute__((ext_vector_type(M)));
+            const auto* q = (const __attribute__((address_space(4))) su32xM*)(uintptr_t)(src + br * a.pitch + sm.col);
+            const su32xM x = *q;
+#pragma unroll
+            for (int j = 0; j < M; j++) sm.s[r][j] = x[j];
+        }
+    }
+    // GOL_SEAM_SMEM 2: the next trip's seam words at the end of this trip, when its row DMAs have filled the lines
+    __device__ __forceinline__ void smem_seam_late() {
+        if constexpr (kSmem && GOL_SEAM_SMEM == 2) {
+            if (sm.on) {
+#pragma unroll
+                for (int r = 0; r < R; r++) smem_seam_row(r, sm.row[r]);
+            }
+        }
+    }
     template <int PAR, int KINDS>
     __device__ __forceinline__ void stage_load_row(int r) {
         if constexpr ((KINDS & 1) == 0) {
@@ -669,14 +689,10 @@ struct StreamWave {
                     br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
                 }
                 rs = src_rs(GOL_AB_WRAPPTR && WRAP_ROWS ? reinterpret_cast<const uint32_t*>(p) : src + br * a.pitch, span_bytes, 8);
-                if constexpr (kSmem) {
-                    if (sm.on) {  // wave-uniform: one scalar load of the row's M seam words
-                        typedef uint32_t su32xM __attribute__((ext_vector_type(M)));
-                        const auto* q = (const __attribute__((address_space(4))) su32xM*)(uintptr_t)(src + br * a.pitch + sm.col);
-                        const su32xM x = *q;
-#pragma unroll
-                        for (int j = 0; j < M; j++) sm.s[r][j] = x[j];
-                    }
+                if constexpr (kSmem && GOL_SEAM_SMEM == 2) {
+                    sm.row[r] = br;
+                } else if constexpr (kSmem) {
+                    if (sm.on) smem_seam_row(r, br);
                 } else if constexpr (kSeam1 && !GOL_AB_NOSEAMDMA) {
                     if (r == 0) stage_load_seam1<PAR>(br);
                 }
@@ -990,6 +1006,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
 #pragma unroll
         for (int r = 0; r < R; r++) NV[r] = 0;
         w.template stage_load<0>();
+        w.smem_seam_late();  // (GOL_SEAM_SMEM 2: trip 0's seam words)
         auto trip = [&](int64_t tt, auto skip, auto mask, auto par) {
             constexpr int PAR = decltype(par)::value;
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
@@ -1061,6 +1078,7 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
                         w.template stage_load_row<1 - PAR, 2>(g / 3);
                 }
             }
+            w.smem_seam_late();  // (GOL_SEAM_SMEM 2)
         };
         using Mask = std::true_type;
         using NoMask = std::false_type;
