@@ -72,14 +72,17 @@ struct Wpb {
 #ifndef GOL_AB_NOSEAMDMA
 #define GOL_AB_NOSEAMDMA 0
 #endif
-// GOL_SEAM_SMEM (round 5, default 1): the seam lane's half-blocks read by the scalar unit -- the R x M seam words of a
-// trip are the same for every lane, so each row's M words come as one s_load into SGPRs with the row's DMAs -- instead
-// of round 4's seam LDS-DMA and its broadcast LDS reads at the trip's top.  The (12, 2) torus pass drops from 164 to
-// 154 VGPRs; 4 interleaved rounds at the bench window (profiles/r5/torus_seam_smem_y.jsonl), us per pass: (12, 2)
-// 431.8 against 434.6, (16, 2) 603.6 against 608.3.  (The board buffer a pass reads is never written during it: the
-// scalar cache, refilled at every dispatch, holds no stale line.)
+// GOL_SEAM_SMEM (round 5, default 2): the seam lane's half-blocks read by the scalar unit -- the R x M seam words of a
+// trip are the same for every lane, so each row's M words come as one s_load into SGPRs -- instead of round 4's seam
+// LDS-DMA and its broadcast LDS reads at the trip's top.  1: each row's s_load with the row's DMAs; 2: the next trip's
+// R s_loads at the end of this trip, after its row DMAs have brought those lines (the seam block sits beside lane 0's)
+// into L2.  The (12, 2) torus pass drops from 164 to 156 VGPRs.  4 interleaved rounds at the bench window, us per
+// pass: 1 against the LDS seam 431.8 / 434.6 (profiles/r5/torus_seam_smem_y.jsonl), but its fills missed L2 (HBM fetch
+// +13 %); 2 against 1: 431.8 / 440.3 with the fetch bytes back at the LDS seam's (torus_seam_late_z.jsonl,
+// fetch_seam_smem*_z.json).  (The board buffer a pass reads is never written during it: the scalar cache, refilled
+// at every dispatch, holds no stale line.)
 #ifndef GOL_SEAM_SMEM
-#define GOL_SEAM_SMEM 1
+#define GOL_SEAM_SMEM 2
 #endif
 // GOL_AB_BSPREAD (A/B): the bounded deep passes spread their row DMAs over the levels as the torus ones do
 #ifndef GOL_AB_BSPREAD
