@@ -585,6 +585,7 @@ def main():
         runner.step(verify_gen - runner.generation)
         torch.cuda.synchronize()
         got_hash, got_pop = runner.hash(), runner.population()
+    runner.close()  # the main leg is done: its buffers go and its engine releases the library (_lib.unload-able)
 
     # One-process C-ABI leg (rank 0), after the main leg; the other ranks wait on a host barrier.
     parts = args.handle_parts if args.handle_parts >= 0 else world

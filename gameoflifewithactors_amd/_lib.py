@@ -142,9 +142,11 @@ SIGNATURES = {
     # test and A/B knobs (csrc/gol_debug.h: internal, not part of the gol.h boundary)
     "gol_debug_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64]),
     "gol_debug_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
+    "gol_debug_option_names": (ctypes.c_char_p, []),
 }
 
 # Names gol_debug_set_option / gol_debug_get_option take (csrc/gol_debug.h); Board.set_option routes them there.
+# The library exports its own list (gol_debug_option_names); tests/test_cpu_host.py checks this one against it.
 DEBUG_OPTIONS = frozenset({"coop_epoch", "coop_spin_limit", "coop_r", "resident_threads", "coop_launch",
                            "lanes_launches"})
 

@@ -16,6 +16,7 @@
 
 #include "../../include/gol/gol.h"
 #include "gol_debug.h"
+#include "gol_debug.h"
 #include "gol_internal.h"
 #include "gol_multi.h"
 
@@ -24,9 +25,14 @@ namespace {
 thread_local std::string g_last_error;
 
 // The test and A/B knobs of gol_debug.h (gol_debug_set_option), refused by gol_set_option with a pointer there.
+// The names gol_debug_set_option / gol_debug_get_option take (csrc/gol_debug.h): ONE list, exported by
+// gol_debug_option_names() so the Python side (_lib.DEBUG_OPTIONS) is checked against it
+constexpr const char* kDebugOptions[] = {"coop_epoch", "coop_spin_limit", "coop_r", "resident_threads", "coop_launch",
+                                         "lanes_launches"};
 bool is_debug_option(const std::string& n) {
-    return n == "coop_epoch" || n == "coop_spin_limit" || n == "coop_r" || n == "resident_threads" ||
-           n == "coop_launch" || n == "lanes_launches";
+    for (const char* d : kDebugOptions)
+        if (n == d) return true;
+    return false;
 }
 
 // Every board call runs on the board's device whatever device the calling thread has current (staging
@@ -331,8 +337,10 @@ int check_valid(gol_board* b) {
         }
     }
     if (b->invalid)
-        return fail(GOL_ERR_HIP, "cooperative pass: a band hand-off timed out (were other kernels occupying CUs?); "
-                                 "the board is invalid until it is overwritten (set_cells, load, seed, clear)");
+        return fail(GOL_ERR_HIP, "persistent pass: a band hand-off timed out -- the pass could not get every CU at "
+                                 "once (another process or stream holds the device); board option \"coop\" 0 "
+                                 "avoids the persistent passes; the board is invalid until it is overwritten "
+                                 "(set_cells, load, seed, clear)");
     return GOL_OK;
 }
 
@@ -846,7 +854,7 @@ int check_strip(const gol_strip* s) {
 
 // StreamArgs of a strip pass (gol_strip_step / gol_strip_plan and the multi board's launches)
 gol::StreamArgs strip_args(const gol_strip* s, int64_t out_begin, int64_t out_end, int32_t split_opt, int64_t seg_opt,
-                           int32_t seam_opt) {
+                           int32_t seam_opt, int32_t split2_opt = 0) {
     gol::StreamArgs a{};
     a.words = s->width / 32;
     a.pitch = s->pitch;
@@ -862,6 +870,7 @@ gol::StreamArgs strip_args(const gol_strip* s, int64_t out_begin, int64_t out_en
     a.split_opt = split_opt;
     a.seg_opt = seg_opt;
     a.seam_opt = seam_opt;
+    a.split2_opt = split2_opt;
     return a;
 }
 
@@ -870,11 +879,11 @@ gol::StreamArgs strip_args(const gol_strip* s, int64_t out_begin, int64_t out_en
 namespace gol {
 
 int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows,
-                    int32_t split_opt, int64_t seg_opt, int32_t seam_opt) {
+                    int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt) {
     if (int rc = check_strip(s)) return rc;
     if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
-    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt);
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt, split2_opt);
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
     if (waves)
@@ -884,7 +893,7 @@ int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_en
 }
 
 int strip_step_opts(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin, int64_t out_end,
-                    hipStream_t stream, int32_t split_opt, int64_t seg_opt, int32_t seam_opt) {
+                    hipStream_t stream, int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt) {
     if (int rc = check_strip(s)) return rc;
     if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
     if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
@@ -900,7 +909,7 @@ int strip_step_opts(const gol_strip* s, const uint32_t* src, uint32_t* dst, int 
         if (lo < -s->ghost || hi > s->rows + s->ghost)
             return fail(GOL_ERR_INVALID, "pass reads rows outside the buffer: ghost must be >= k");
     }
-    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt);
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt, split2_opt);
     GOL_HIP(gol::launch_stream_step(src, dst, a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0, stream));
     return GOL_OK;
 }
@@ -1467,11 +1476,20 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
     else
         return fail(GOL_ERR_INVALID, "unknown option '" + n + "'");
     // a multi-part board runs every strip launch with the streaming options (the other passes never run there)
-    if (b->multi) b->multi->set_stream_options(o.split, o.seg_rows, o.seam);
+    if (b->multi) b->multi->set_stream_options(o.split, o.seg_rows, o.seam, o.split2);
     return GOL_OK;
 }
 
 // Test and A/B knobs (csrc/gol_debug.h; VERDICT round 4 item 3: kept out of gol.h's option list).
+const char* gol_debug_option_names(void) {
+    static const std::string names = [] {
+        std::string r;
+        for (const char* d : kDebugOptions) r += (r.empty() ? "" : ",") + std::string(d);
+        return r;
+    }();
+    return names.c_str();
+}
+
 int gol_debug_set_option(gol_board* b, const char* name, int64_t value) {
     if (int rc = check_board(b)) return rc;
     if (!name) return fail(GOL_ERR_INVALID, "null option name");

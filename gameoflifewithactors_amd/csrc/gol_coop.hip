@@ -172,9 +172,10 @@ __device__ __forceinline__ int ld_granules(const uint64_t* const (&src)[R], uint
 // 16-byte hand-off (round 5): a lane's granules in pairs, as 16-byte write-through stores and 16-byte sc1 polls
 // (two {word, tag} granules per access, each 8-byte half written by ONE store: MI355X_MICROARCH.md "Valid forms", R2
 // halves) -- half the hand-off's memory instructions at M = 2 and whole 1 KB runs per wave instruction.  Rows of an
-// even word count per lane (M = 2, 4) use it: 4096^2 0.69 -> 0.58 us/generation with the lean loop below, 8192 x
-// 4096 1.56 -> 1.01 (profiles/r5/coop_variants_ab_d.log, coop_poll_delay_ab_g.log).  Rejected A/B variants, same
-// logs: two poll rounds kept in flight (slower at 4096^2: the compiler serialises the rounds' register copies),
+// even word count per lane (M = 2, 4) use it: 4096^2 0.693 -> 0.582 us/generation (means of 3 interleaved rounds,
+// profiles/r5/coop_g16_ab_b.jsonl / .txt), 0.572 with the lean loop below (coop_variants_ab_d, "g1posl"); 8192 x 4096
+// 1.573 -> 1.009 with the 8192-wide poll delay (coop_variants_ab_d "base" -> coop_poll_delay_ab_g "coopd24").
+// Rejected A/B variants, same files: two poll rounds kept in flight (slower at 4096^2: the compiler serialises the rounds' register copies),
 // bands mapped XCD by XCD so neighbours share an L2 (profiles/r5/ab_xcd_h.log: 8192 x 4096 1.27 vs 1.01), 8-byte
 // buffer granules for M = 1 (level with the atomic form).
 constexpr int kAuxSc1 = 16;  // buffer instruction cache policy: sc1 (gfx950)

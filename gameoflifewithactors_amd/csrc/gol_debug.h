@@ -27,6 +27,8 @@ extern "C" {
 
 int gol_debug_set_option(gol_board* b, const char* name, int64_t value);
 int gol_debug_get_option(gol_board* b, const char* name, int64_t* value);
+/* The names above, comma-separated (the library's own list: _lib.DEBUG_OPTIONS is tested against it). */
+const char* gol_debug_option_names(void);
 
 #ifdef __cplusplus
 }

@@ -47,8 +47,8 @@ int stream_max_k(int ilv);
 int stream_largest_k(int64_t n, int cap, int ilv);
 // rag_bits: cells in the last word of a ragged row (words = ceil(W / 32), ilv 1), 0 for whole-word rows
 int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0);
-int stream_pair_split(int k, int ilv, bool bounded, bool wrap);
-int stream_split2(int k, int ilv, bool bounded, bool wrap);
+int stream_pair_split(int k, int ilv, bool bounded, bool wrap, bool single);
+int stream_split2(int k, int ilv, bool bounded, bool wrap, bool single);
 int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_bits = 0);
 // fills nstrips / nsegs / seg (one balanced round of resident waves unless a.seg_opt -- the "seg_rows" option -- is set)
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);

@@ -141,7 +141,7 @@ int MultiBoard::set_transport(int transport) {
 // gol_strip_step with the board's streaming options (gol_capi.cpp)
 int MultiBoard::strip_step(const gol_strip& s, const uint32_t* src, uint32_t* dst, int k, int64_t b, int64_t e,
                            hipStream_t st) const {
-    return strip_step_opts(&s, src, dst, k, b, e, st, split_opt_, seg_opt_, seam_opt_);
+    return strip_step_opts(&s, src, dst, k, b, e, st, split_opt_, seg_opt_, seam_opt_, split2_opt_);
 }
 
 int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* devices, int n, int tblock, int ilv) {
@@ -454,8 +454,8 @@ int MultiBoard::pass(int k, std::vector<PassTimer>* timers) {
         if (lo < hi) {
             // leave room on the device for the two edge bands, which start as soon as the ghost rows land
             int64_t w0 = 0, w1 = 0;
-            GOL_MRC(strip_plan_opts(&p.s, k, 0, lo, &w0, nullptr, split_opt_, seg_opt_, seam_opt_));
-            GOL_MRC(strip_plan_opts(&p.s, k, hi, rows, &w1, nullptr, split_opt_, seg_opt_, seam_opt_));
+            GOL_MRC(strip_plan_opts(&p.s, k, 0, lo, &w0, nullptr, split_opt_, seg_opt_, seam_opt_, split2_opt_));
+            GOL_MRC(strip_plan_opts(&p.s, k, hi, rows, &w1, nullptr, split_opt_, seg_opt_, seam_opt_, split2_opt_));
             gol_strip s = p.s;
             s.spare_waves = (int32_t)std::min<int64_t>(w0 + w1, 1 << 20);
             GOL_MRC(strip_step(s, src, dst, k, lo, hi, p.compute));

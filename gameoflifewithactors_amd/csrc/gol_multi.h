@@ -27,11 +27,12 @@
 namespace gol {
 
 int api_fail(int code, const std::string& msg);  // sets gol_last_error (gol_capi.cpp)
-// gol_strip_step / gol_strip_plan with a board's streaming options ("split", "seg_rows", "seam"; gol_capi.cpp)
+// gol_strip_step / gol_strip_plan with a board's streaming options ("split", "seg_rows", "seam", "split2";
+// gol_capi.cpp)
 int strip_step_opts(const gol_strip* s, const uint32_t* src, uint32_t* dst, int k, int64_t out_begin, int64_t out_end,
-                    hipStream_t stream, int32_t split_opt, int64_t seg_opt, int32_t seam_opt);
+                    hipStream_t stream, int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt = 0);
 int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t* waves, int64_t* seg_rows,
-                    int32_t split_opt, int64_t seg_opt, int32_t seam_opt);
+                    int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt = 0);
 
 // The halo messages of one pass, in the order each part issues them (include/gol/gol.h gol_xfer): part r sends its
 // top k owned rows to `up` and its bottom k rows to `down`, then receives the down neighbour's top rows below its
@@ -78,11 +79,13 @@ class MultiBoard {
     // halo transport: GOL_TRANSPORT_PEER (default) or GOL_TRANSPORT_RCCL (creates the communicators on first use;
     // GOL_ERR_UNSUPPORTED when a device repeats or RCCL is unavailable, and the board keeps its transport)
     int set_transport(int transport);
-    // streaming-pass options of the board (gol_set_option "split", "seg_rows", "seam"), applied to every strip launch
-    void set_stream_options(int32_t split_opt, int64_t seg_opt, int32_t seam_opt) {
+    // streaming-pass options of the board (gol_set_option "split", "seg_rows", "seam", "split2"), applied to every
+    // strip launch
+    void set_stream_options(int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt) {
         split_opt_ = split_opt;
         seg_opt_ = seg_opt;
         seam_opt_ = seam_opt;
+        split2_opt_ = split2_opt;
     }
 
     int parts() const { return (int)parts_.size(); }
@@ -107,7 +110,7 @@ class MultiBoard {
     bool rccl_ = false;       // the transport in use
     bool comms_ = false;      // RCCL communicators exist (parts_[i].comm)
     bool distinct_ = false;   // every part has its own device
-    int32_t split_opt_ = 0, seam_opt_ = 0;
+    int32_t split_opt_ = 0, seam_opt_ = 0, split2_opt_ = 0;
     int64_t seg_opt_ = 0;
     std::string transport_note_;
     int64_t W_ = 0, H_ = 0;

@@ -1281,14 +1281,16 @@ int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_b
 // equal segments it finishes early and leaves the younger alone at the single-wave issue rate
 // (tools/tail.py: 65536^2, K = 16 -- waves 0-3 of every workgroup busy 489 us, waves 4-7 747 us).
 // A board's "split" option (gol_set_option) overrides it for experiments.
-int stream_pair_split(int k, int ilv, bool bounded, bool wrap) {
+int stream_pair_split(int k, int ilv, bool bounded, bool wrap, bool single) {
     if (kWavesPerBlock < 8) return 0;
     // Round 5, with the middle wave's share set apart (stream_split2), at the bench window (generation 300+), 4
     // interleaved rounds (profiles/r5/split2_confirm_g.jsonl, us per pass, mean): single-board torus (12, 2) 0.66 / 0.76
     // 442.5 against 0.70 / geometric 445.8; bounded (12, 2) 0.60 / 0.72 431.0 against 0.64 / geometric 436.0.  The
     // per-role tails of a stamped build (profiles/r5/split2_tails_f.jsonl): torus roles ending at 439 / 378 / 436 us with
-    // geometric shares, 440 / 417 / 430 with 0.68 / 0.76.  (The ghost-row strips of N > 1 keep their measured split.)
-    if (bounded && ilv == 2 && k == 12) return (int)(0.60 * 65536);
+    // geometric shares, 440 / 417 / 430 with 0.68 / 0.76.  Both retunes were measured on single boards only, so the
+    // ghost-row strips of N > 1 keep round 4's measured split on either boundary (`single`: one strip holding the whole
+    // board, ghost 0): torus strips fall through to 0.70 below, bounded strips keep 0.64.
+    if (bounded && ilv == 2 && k == 12) return (int)((single ? 0.60 : 0.64) * 65536);
     if (!bounded && wrap && ilv == 2 && k == 12) return (int)(0.66 * 65536);
     // measured at 65536^2 (profiles/r1/split_sweep*.log, two boxes): the deep passes gain 3-9 %; the
     // shallow ones (short, memory-bound trips) are left unpaired
@@ -1350,15 +1352,16 @@ static bool seam_applies(const StreamArgs& a, int k, bool bounded) {
 // segments no shorter than 2K rows (pipeline fill cost).  a.split_opt / a.seg_opt / a.seam_opt (a board's "split" /
 // "seg_rows" / "seam" options) override the split, the segment length and the geometry for experiments.
 // Three-wave groups: the middle wave's share of the two younger waves' rows (1/65536), 0 = geometric.
-int stream_split2(int k, int ilv, bool bounded, bool wrap) {
-    if (kWavesPerBlock < 8 || ilv != 2 || k != 12) return 0;  // (12, 2): the one three-wave group variant
+int stream_split2(int k, int ilv, bool bounded, bool wrap, bool single) {
+    if (kWavesPerBlock < 8 || ilv != 2 || k != 12 || !single) return 0;  // (12, 2) single boards: see stream_pair_split
     if (bounded) return (int)(0.72 * 65536);
     return wrap ? (int)(0.76 * 65536) : 0;
 }
 
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap) {
-    a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded, wrap));
-    a.split2 = a.split2_opt > 0 ? a.split2_opt : stream_split2(k, a.ilv, bounded, wrap);
+    const bool single = a.ghost == 0 && a.rows == a.height;  // the whole board in one buffer (not a ghost-row strip)
+    a.split = a.split_opt > 0 ? a.split_opt : (a.split_opt < 0 ? 0 : stream_pair_split(k, a.ilv, bounded, wrap, single));
+    a.split2 = a.split2_opt > 0 ? a.split2_opt : stream_split2(k, a.ilv, bounded, wrap, single);
     const int64_t nblocks = a.words / a.ilv;
     a.seam = seam_applies(a, k, bounded) ? 1 : 0;
     a.rem = 0;

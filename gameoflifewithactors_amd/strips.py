@@ -72,6 +72,19 @@ class HipEngine:
         _lib.hold(self)  # _lib.unload() refuses while this engine can still call the library
         self.device = device
 
+    def close(self) -> None:
+        """Drop this engine's hold on the library: _lib.unload() -- the documented way to unregister
+        the device code before exit under rocprofv3 (DESIGN.md 6) -- refuses while an engine holds it.  Idempotent;
+        the engine must not be used afterwards."""
+        _lib.release(self)
+        self.lib = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     def ilv_for(self, width: int) -> int:
         return int(self.lib.gol_default_ilv(width))
 
@@ -150,6 +163,7 @@ class StripRunner:
         if world > 1 and rows < k:
             raise ValueError(f"strip of {rows} rows is thinner than the temporal block k={k}")
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._own_engine = engine is None  # close() releases an engine this runner created, not a caller's
         self.engine = engine if engine is not None else HipEngine(self.device)
         single = world == 1
         ilv = getattr(self.engine, "ilv_for", lambda w: 1)(width)
@@ -170,6 +184,23 @@ class StripRunner:
         self.up = (rank - 1) % world if (boundary == TORUS or rank > 0) else None
         self.down = (rank + 1) % world if (boundary == TORUS or rank < world - 1) else None
         self.exchanger = exchanger if exchanger is not None else DistExchange(group)
+
+    def close(self) -> None:
+        """Wait for this strip's streams, free its buffers and release the engine it created (HipEngine.close), so
+        _lib.unload() can run after the strip is done.  Idempotent."""
+        if getattr(self, "bufs", None) is None:
+            return
+        self.compute_stream.synchronize()
+        self.edge_stream.synchronize()
+        self.bufs = None
+        if self._own_engine and hasattr(self.engine, "close"):
+            self.engine.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # ---------------------------------------------------------------- state
     def seed_splitmix(self, seed: int) -> None:
@@ -347,6 +378,16 @@ class LocalBoard:
     def _sync_all(self):
         for r in self.runners:
             r.compute_stream.synchronize()
+
+    def close(self) -> None:
+        for r in self.runners:
+            r.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def step_pass(self, k: int | None = None) -> None:
         self._sync_all()  # every strip's current buffer is final before anyone copies from it

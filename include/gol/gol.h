@@ -179,14 +179,14 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  *   "seam" 0 | -1                streaming pass on a torus: seam strips where they apply (-1: halo-lane strips)
  *   "transport" 1 | 2            multi-part boards: halo rows by peer copies (1) or RCCL (2, distinct devices;
  *                                GOL_ERR_UNSUPPORTED otherwise); GOL_ERR_UNSUPPORTED on a single board
- *   ("split", "seg_rows" and "seam" apply to every strip launch of a multi-part board as well)
+ *   ("split", "split2", "seg_rows" and "seam" apply to every strip launch of a multi-part board as well)
  *   "ragged_ring" 1 | 2 | 0      ragged boards on the streaming pass as block rows in the aligned layouts (torus: ring
  *                                rows; bounded: column-masked rows) from 3 * 2^26 cells (1), on every size (2), or
  *                                never (0: ilv-1 rows)
  *   "ragged_stream" 1 | 0        boards of any width beyond the cooperative pass: the streaming pass on scratch
  *                                words (0: the per-generation byte step)
  *   "coop_poll_delay" -1 | 0..4096  s_sleep periods before a hand-off's first poll (-1: on the cooperative pass 0 for
- *                                4096-cell rows, 4 for narrower ones, 24 for 8192; 8 on the rows-on-lanes pass)
+ *                                4096-cell rows, 4 for narrower ones, 24 for every width above 4096; 8 on the rows-on-lanes pass)
  *   "lanes" 2 | 1 | 0            rows-on-lanes band pass in place of the cooperative one (packed single boards whose
  *                                width splits into 128/256/512/1024-column windows, coop_k <= 10, calls of >= 2 k
  *                                generations, every band resident at once): 2 = on the sizes it
@@ -197,7 +197,12 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
  * (Test and A/B knobs -- spin limits, tag epochs, launch API -- are not board options: they live behind
  * gol_debug_set_option in the library's internal header csrc/gol_debug.h.)
  * The persistent passes (cooperative, rows-on-lanes) of all boards of a process are serialised per device, so two
- * handles stepping at once from two threads never split the CUs between two such grids. */
+ * handles stepping at once from two threads never split the CUs between two such grids.  The serialisation is per
+ * PROCESS: a second process stepping a mid-size board on the same GPU at the same time can hold CUs a persistent grid
+ * needs.  Its bands then wait out the spin limit (~2 s), the call's board is left wrong, and the next
+ * gol_synchronize or readback returns GOL_ERR_HIP with gol_last_error() naming that cause ("a band hand-off timed
+ * out -- the pass could not get every CU at once ...").  Set "coop" 0 on boards that share a GPU with other
+ * processes: every generation then runs on the ordinary (non-persistent) passes. */
 int gol_set_option(gol_board* b, const char* name, int64_t value);
 int gol_get_option(gol_board* b, const char* name, int64_t* value);
 

@@ -44,6 +44,17 @@ def test_library_exports_every_declared_symbol():
         assert name in _lib.SIGNATURES, f"_lib.SIGNATURES lacks a binding for {name}"
 
 
+def test_debug_option_list_matches_the_library():
+    """the test knobs are listed once in the library (csrc/gol_capi.cpp kDebugOptions, exported by
+    gol_debug_option_names); the Python routing set _lib.DEBUG_OPTIONS must be exactly that list, or a knob would be
+    sent to gol_set_option (GOL_ERR_INVALID) without any test noticing."""
+    from gameoflifewithactors_amd import _lib
+
+    names = _lib.load().gol_debug_option_names().decode().split(",")
+    assert len(names) == len(set(names))
+    assert set(names) == set(_lib.DEBUG_OPTIONS)
+
+
 def test_layout_choice():
     from gameoflifewithactors_amd import _lib
 
@@ -80,6 +91,35 @@ def test_library_unloads_and_reloads():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "gfx950" in r.stdout
+
+
+def test_strip_engine_close_lets_the_library_unload():
+    """a HipEngine (and a StripRunner that created one) holds the library; close() releases it, so
+    _lib.unload() works once the strips are done.  CPU strips (no device memory), in a child process."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import torch\n"
+            "from gameoflifewithactors_amd import _lib\n"
+            "from gameoflifewithactors_amd.strips import HipEngine, StripRunner\n"
+            "e = HipEngine(torch.device('cpu'))\n"
+            "try:\n    _lib.unload(); raise SystemExit('unload with a live engine')\n"
+            "except _lib.GolError: pass\n"
+            "e.close(); e.close(); _lib.unload(); assert _lib._lib is None\n"
+            "class Eng(HipEngine):\n"
+            "    def alloc(self, geom, stream): return torch.zeros((geom.buffer_rows, geom.pitch), dtype=torch.int32)\n"
+            "with Eng(torch.device('cpu')) as own:\n"
+            "    r = StripRunner(64, 16, 0, 1, device=torch.device('cpu'), engine=own)\n"
+            "    r.close()  # a caller's engine stays held until the caller closes it\n"
+            "    assert own in _lib._holders\n"
+            "assert own not in _lib._holders\n"
+            "_lib.unload(); assert _lib._lib is None\n"
+            "print('ok')\n") % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert "ok" in r.stdout
 
 
 def test_arch_check_accepts_only_gfx950():
@@ -262,19 +302,22 @@ def test_seam_remainder_waves_stay_inside_the_buffer(words, ilv, k):
                     assert 0 <= row < buf_rows, (rows, wrap, (b, e), plan, r, sy, j, row)
 
 
-@pytest.mark.parametrize("wrap,boundary,want", [(True, 0, (0.66, 0.76)), (False, 1, (0.60, 0.72)), (False, 0, (0.70, 0.0))])
-def test_stream_plan_group_split_defaults(wrap, boundary, want):
+@pytest.mark.parametrize("wrap,boundary,single,want", [(True, 0, True, (0.66, 0.76)), (False, 1, True, (0.60, 0.72)),
+                                                       (False, 0, False, (0.70, 0.0)), (False, 1, False, (0.64, 0.0))])
+def test_stream_plan_group_split_defaults(wrap, boundary, single, want):
     """Round 5: the (12, 2) deep pass's three-wave SIMD groups split a segment by two ratios (split, split2), tuned
-    per variant at the bench window (profiles/r5/split2_confirm_g.jsonl): single-board torus 0.66 /
-    0.76, bounded 0.60 / 0.72; ghost-row torus strips keep round 4's single ratio 0.70 (split2 0: geometric)."""
+    per variant at the bench window on SINGLE boards (profiles/r5/split2_confirm_g.jsonl): torus 0.66 /
+    0.76, bounded 0.60 / 0.72.  Ghost-row strips (N > 1) were never measured at those values, so they keep round 4's
+    single ratio on both boundaries: torus 0.70, bounded 0.64 (split2 0: geometric)."""
     import ctypes
 
     from gameoflifewithactors_amd import _lib
 
     lib = _lib.load()
     rows, k, words = 65536, 12, 2048
-    ghost = 0 if wrap else k
-    strip = _lib.Strip(words * 32, rows if wrap else rows * 2, 0, rows, ghost, words, boundary, 1 if wrap else 0, 2, 0)
+    ghost = 0 if single else k
+    height = rows if single else rows * 2
+    strip = _lib.Strip(words * 32, height, 0, rows, ghost, words, boundary, 1 if wrap else 0, 2, 0)
     plan = (ctypes.c_int64 * 10)()
     assert lib.gol_strip_plan_ex(ctypes.byref(strip), k, 0, rows, plan, 10) == 0, lib.gol_last_error()
     assert plan[8] == int(want[0] * 65536) and plan[9] == int(want[1] * 65536), list(plan)
