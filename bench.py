@@ -60,6 +60,80 @@ def valu_slots_per_word_gen(ilv: int) -> float:
     return 9 + 8 / ilv
 
 
+def _rccl_version():
+    """RCCL's version as the torch build links it ("2.27.7"), or None (no RCCL in this torch)."""
+    try:
+        import torch
+
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 -- a report field, not a failure
+        return None
+
+
+def _mapped_rccl():
+    """The librccl this process has mapped (/proc/self/maps), or None: which RCCL actually served the group."""
+    try:
+        with open("/proc/self/maps") as f:
+            libs = sorted({line.split()[-1] for line in f if "librccl" in line and "/" in line})
+        return libs or None
+    except OSError:
+        return None
+
+
+def _device_identity(dev) -> dict:
+    """{device, pci_bus_id, name} of this rank's GPU (hipDeviceProp_t through torch), or nulls on a CPU strip."""
+    import torch
+
+    if dev is None or not torch.cuda.is_available():
+        return {"device": None, "pci_bus_id": None, "name": None}
+    p = torch.cuda.get_device_properties(dev)
+    bus = getattr(p, "pci_bus_id", None)
+    pci = None
+    if bus is not None:
+        pci = "%04x:%02x:%02x.0" % (getattr(p, "pci_domain_id", 0), bus, getattr(p, "pci_device_id", 0))
+    return {"device": int(dev), "pci_bus_id": pci, "name": p.name}
+
+
+def multi_gpu_report(runner, dev, backend: str, host_group=None, probe_passes: int = 4) -> dict:
+    """What an N > 1 line needs to answer "did RCCL see N ranks, on which GPUs, and what did the halo cost?"
+    (VERDICT round 5, item 4).  Collective: every rank calls it, after the timed region; rank 0 gets the full dict.
+
+    * `process_group_size`: torch.distributed's world size; `allreduce_rank_count`: the sum of a 1 from every rank
+      all-reduced over the data-path group (RCCL when the backend is nccl) -- N only if RCCL connected all N ranks.
+    * `rccl_version` / `rccl_library`: the RCCL torch links and the librccl mapped into this process.
+    * `ranks`: per rank (all-gathered over the host group) its device, PCI bus id, device name, host, and the main
+      leg's per-phase pass timing: `probe_passes` passes exactly as timed (StripRunner.timed_pass, HIP events):
+      interior launch end, halo-exchange wait (edge stream released) and edge-band end, from the pass start, in us.
+    * `edge_wait_us_max`: the slowest rank's mean halo wait.
+    The probe passes advance the board (the self-check steps on from wherever it is)."""
+    import torch
+    import torch.distributed as dist
+
+    probes = [runner.timed_pass() for _ in range(probe_passes)]
+    timing = {key: round(sum(p[key] for p in probes) / len(probes), 2) for key in probes[0]} if probes else {}
+    cuda = backend == "nccl"
+    one = torch.ones(1, dtype=torch.int64, device=torch.device("cuda", dev) if cuda else "cpu")
+    dist.all_reduce(one)  # over the default (data-path) group: RCCL for nccl
+    me = {"rank": dist.get_rank(), **_device_identity(dev if (dev is not None and torch.cuda.is_available()) else None),
+          "host": platform.node(), "pass_timing_us": timing, "generations_per_pass": runner.k}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me, group=host_group)
+    waits = [r["pass_timing_us"].get("edge_wait_us") for r in ranks if r and r["pass_timing_us"]]
+    return {
+        "backend": backend,
+        "rccl_version": _rccl_version() if cuda or torch.cuda.is_available() else None,
+        "rccl_library": _mapped_rccl(),
+        "process_group_size": dist.get_world_size(),
+        "allreduce_rank_count": int(one.item()),
+        "ranks": ranks,
+        "edge_wait_us_max": max(waits) if waits and None not in waits else None,
+        "probe_passes": probe_passes,
+        "timing": "StripRunner.timed_pass: HIP events on the strip's compute and edge streams, from the pass start "
+                  "(before the halo exchange is posted); means over the probe passes, run after the timed region",
+    }
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -521,6 +595,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kernel_s = float(t[0]), float(t[1])
 
+    # N > 1: the ranks, their GPUs, RCCL's view of the group and the main leg's per-rank halo figures, after the
+    # timed region (every rank takes part)
+    multi = multi_gpu_report(runner, dev, args.dist_backend, host_group) if world > 1 else None
+
     # Memory-side reference point, outside the timed region: the same board streamed by K = 1 passes (the
     # halo-free streaming kernel), HIP events on the compute stream.  Single GPU only.
     k1 = None
@@ -664,6 +742,8 @@ def main():
             "hip_runtime": _lib.hip_runtimes(),
             "device_code": fingerprint,
         }
+        if multi is not None:
+            result["multi_gpu"] = multi
         if verify is not None:
             result["verify"] = verify
         if handle is not None:

@@ -26,6 +26,7 @@ device-to-device; `LocalBoard` uses it to run N strips on the GPUs of one proces
 from __future__ import annotations
 
 import ctypes
+import time
 from dataclasses import dataclass
 
 import torch
@@ -225,14 +226,16 @@ class StripRunner:
         with _stream_ctx(self.compute_stream):
             return self.exchanger.post(self, self.bufs[self.cur], k)
 
-    def compute(self, reqs, k: int | None = None) -> None:
-        """Interior rows (overlapping the exchange), wait, then the boundary rows; swap buffers."""
+    def compute(self, reqs, k: int | None = None, marks: dict | None = None) -> None:
+        """Interior rows (overlapping the exchange), wait, then the boundary rows; swap buffers.  `marks` (timed_pass):
+        timing marks recorded after the interior launch, at the edge stream's release and after the edge bands."""
         k = self.k if k is None else k
         src, dst = self.bufs[self.cur], self.bufs[self.cur ^ 1]
         h = self.geom.rows
         s = self.compute_stream
         if self.world == 1:
             self.engine.step(self.geom, src, dst, k, 0, h, s)
+            _mark(marks, "interior", s)
         else:
             lo, hi = min(k, h), max(h - k, min(k, h))
             e = self.edge_stream
@@ -242,11 +245,14 @@ class StripRunner:
             plan = getattr(self.engine, "plan_waves", None)
             spare = plan(self.geom, k, 0, lo) + plan(self.geom, k, hi, h) if plan else 0
             self.engine.step(self.geom, src, dst, k, lo, hi, s, spare_waves=spare)
+            _mark(marks, "interior", s)
             with _stream_ctx(e):
                 for r in reqs:
                     r.wait()  # the edge stream waits for the received ghost rows
+            _mark(marks, "go", e)
             self.engine.step(self.geom, src, dst, k, 0, lo, e)
             self.engine.step(self.geom, src, dst, k, hi, h, e)
+            _mark(marks, "edge", e)
             _wait_stream(s, e)  # the pass ends when both streams are done
         self.cur ^= 1
         self.generation += k
@@ -254,6 +260,27 @@ class StripRunner:
     def step_pass(self, k: int | None = None) -> None:
         """Advance k (default self.k) generations: exchange || interior, then boundary rows."""
         self.compute(self.post_exchange(k), k)
+
+    def timed_pass(self, k: int | None = None) -> dict:
+        """One pass exactly as step_pass, timed per phase from its start (before the halo exchange is posted): to the
+        end of the interior launch, to the edge stream's release (the ghost rows landed: the halo-exchange wait) and
+        to the end of the two edge bands (the keys of the handle leg's gol_pass_timing).  HIP events on the streams
+        of a GPU strip (synchronised after the pass, not inside it); the host clock on a CPU strip.  bench.py runs a
+        few of these after its timed region for the per-rank halo figures of an N > 1 line."""
+        marks: dict = {}
+        _mark(marks, "start", self.compute_stream)
+        self.compute(self.post_exchange(k), k, marks)
+        start = marks.pop("start")
+        if isinstance(start, float):
+            us = {n: (t - start) * 1e6 for n, t in marks.items()}
+        else:
+            torch.cuda.synchronize(self.device)
+            us = {n: start.elapsed_time(ev) * 1e3 for n, ev in marks.items()}
+        out = {"interior_us": round(us["interior"], 2)}
+        if "go" in us:
+            out["edge_wait_us"] = round(us["go"], 2)
+            out["edge_done_us"] = round(us["edge"], 2)
+        return out
 
     def step(self, generations: int) -> None:
         while generations > 0:
@@ -396,6 +423,27 @@ class LocalBoard:
         for r, q in zip(self.runners, reqs):
             r.compute(q, k)
 
+    def timed_pass(self, k: int | None = None) -> dict:
+        """One pass exactly as step_pass, timed per phase from its start (before the halo exchange is posted): to the
+        end of the interior launch, to the edge stream's release (the ghost rows landed: the halo-exchange wait) and
+        to the end of the two edge bands (the keys of the handle leg's gol_pass_timing).  HIP events on the streams
+        of a GPU strip (synchronised after the pass, not inside it); the host clock on a CPU strip.  bench.py runs a
+        few of these after its timed region for the per-rank halo figures of an N > 1 line."""
+        marks: dict = {}
+        _mark(marks, "start", self.compute_stream)
+        self.compute(self.post_exchange(k), k, marks)
+        start = marks.pop("start")
+        if isinstance(start, float):
+            us = {n: (t - start) * 1e6 for n, t in marks.items()}
+        else:
+            torch.cuda.synchronize(self.device)
+            us = {n: start.elapsed_time(ev) * 1e3 for n, ev in marks.items()}
+        out = {"interior_us": round(us["interior"], 2)}
+        if "go" in us:
+            out["edge_wait_us"] = round(us["go"], 2)
+            out["edge_done_us"] = round(us["edge"], 2)
+        return out
+
     def step(self, generations: int) -> None:
         while generations > 0:
             k = self.k if generations >= self.k else self.runners[0]._largest_k(generations)
@@ -449,6 +497,18 @@ class _NullCtx:
 
     def __exit__(self, *a):
         return False
+
+
+def _mark(marks, name: str, stream) -> None:
+    """A timing mark of timed_pass: a timing event recorded on `stream` (GPU strip), else the host clock."""
+    if marks is None:
+        return
+    if isinstance(stream, torch.cuda.Stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        marks[name] = ev
+    else:
+        marks[name] = time.perf_counter()
 
 
 def _wait_stream(waiter, other) -> None:

@@ -131,6 +131,41 @@ def test_bench_two_ranks_over_gloo():
     h = r["handle_leg"]
     assert h["value"] > 0 and h["strips"] == 2 and len(h["pass_timing_us"]) == 2, h
     assert all(t["edge_done_us"] >= t["edge_wait_us"] >= 0 for t in h["pass_timing_us"])
+    _assert_multi_gpu_report(r["multi_gpu"], 2, "gloo")
+
+
+def _assert_multi_gpu_report(m, world, backend):
+    """the N > 1 line's group, devices and the main leg's per-rank halo figures."""
+    assert m["backend"] == backend and m["process_group_size"] == world and m["allreduce_rank_count"] == world, m
+    assert m["rccl_version"], m  # the RCCL torch links (reported on a gloo rehearsal too)
+    assert [x["rank"] for x in m["ranks"]] == list(range(world))
+    for x in m["ranks"]:
+        assert x["device"] == 0 and x["pci_bus_id"] and x["name"], x  # every rank on this box's one GPU
+        t = x["pass_timing_us"]
+        assert t["edge_done_us"] >= t["edge_wait_us"] >= 0 and t["interior_us"] > 0, t
+    assert m["edge_wait_us_max"] == max(x["pass_timing_us"]["edge_wait_us"] for x in m["ranks"])
+
+
+def test_bench_two_ranks_strong_scaling_form_over_gloo():
+    """The strong-scaling form (--board N: config 4's fixed board split over the ranks) carries the same N > 1
+    fields.  A 16384^2 board here, two ranks on this GPU over gloo."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29617", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--board", "16384", "--dist-backend", "gloo", "--no-cpu-baseline",
+           "--handle-parts", "0", "--no-verify"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["scaling"] == "strong" and r["config"]["width"] == 16384 and r["config"]["height"] == 16384
+    _assert_multi_gpu_report(r["multi_gpu"], 2, "gloo")
 
 
 def test_262144_board_strips_match_single_board():

@@ -124,3 +124,61 @@ def test_multi_rank_check_catches_a_mispaired_exchange(broken):
         assert p.exitcode == 0
     assert all(v is not None for _, v in res), "a rank failed"
     assert all(v["ok"] is (not broken) for _, v in res), res
+
+
+def _report_worker(rank, world, port, q):
+    import json
+    import sys
+
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = None
+    try:
+        from strip_oracle_engine import OracleEngine
+
+        import bench
+        from gameoflifewithactors_amd.strips import StripRunner
+
+        r = StripRunner(256, 48, 0, 4, rank=rank, world=world, device=torch.device("cpu"), engine=OracleEngine())
+        r.seed_splitmix(0x5EED)
+        r.step(8)
+        rep = bench.multi_gpu_report(r, None, "gloo", None, probe_passes=2)
+        out = json.dumps(rep)  # the line is JSON: the report must serialise as it stands
+        assert r.generation == 8 + 2 * 4  # the probe passes advanced the board
+    finally:
+        q.put((rank, out))
+        dist.destroy_process_group()
+
+
+def test_multi_gpu_report_json_contract():
+    """an N > 1 bench line says how many ranks the data-path group connected (all-reduce of
+    a 1 per rank), which RCCL, which device and PCI bus each rank ran on, and the main leg's per-rank halo-exchange
+    wait and edge-band time (StripRunner.timed_pass).  World 2 over gloo on CPU strips: the fields and their shape."""
+    import json
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v is not None for _, v in res), "a rank failed"
+    for _, v in res:
+        rep = json.loads(v)
+        assert rep["backend"] == "gloo"
+        assert rep["process_group_size"] == world and rep["allreduce_rank_count"] == world
+        assert "rccl_version" in rep and "rccl_library" in rep
+        assert [x["rank"] for x in rep["ranks"]] == list(range(world))
+        for x in rep["ranks"]:
+            assert set(x) >= {"rank", "device", "pci_bus_id", "name", "host", "pass_timing_us", "generations_per_pass"}
+            t = x["pass_timing_us"]
+            assert t["edge_done_us"] >= t["edge_wait_us"] >= 0 and t["interior_us"] >= 0, t
+        assert rep["edge_wait_us_max"] == max(x["pass_timing_us"]["edge_wait_us"] for x in rep["ranks"])
