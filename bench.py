@@ -32,19 +32,32 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# depths raced on the box before the timed region (default; --no-autotune skips it), per layout (ilv)
+# depths raced on the box before the timed region (default; --no-autotune skips it), per layout (ilv); ilv 4 (the
+# level-pipelined pass) runs its one default depth
 AUTOTUNE = {2: [12, 16], 1: [24, 32]}
 
 
-def default_depth(lib, ilv: int, world: int, boundary: str) -> int:
-    """Fixed default temporal depth, so the bench line and a rocprof trace of the same command run the same
-    kernel.  Torus, single board or ghost-row strips (N > 1): the engine default K = 12 at M = 2 (12-wave
-    workgroups).  Over the whole 10k-generation job it beats K = 16 on both: single board 116.4k vs 109.5k
-    GCUPS (profiles/r1/bench_k_ab.log), strips 113.7-114.1k vs 99.2-101.0k (strip_k_ab.log); K = 16 wins only
-    on the first passes of a fresh board (ghost_ab2.log).  Bounded boards too since round 3's staged passes:
-    127.5k vs 119.2k GCUPS over the whole job (profiles/r3/bench_bounded_job_d.log)."""
-    del boundary
-    return int(lib.gol_default_tblock(ilv))
+def default_layout(lib, width: int, rows: int, boundary: int) -> tuple[int, int]:
+    """The engine's (ilv, K) for a strip of `rows` rows (gol_default_layout), fixed so the bench line and a rocprof
+    trace of the same command run the same kernel.  Torus strips of >= 2^30 cells (the 65536^2 board per GPU): ilv 4
+    and K = 32 on the level-pipelined pass (gol_pipe.hip).  Otherwise the streaming pass's K = 12 at
+    M = 2 (12-wave workgroups): over the whole 10k-generation job it beat K = 16 on the single board (116.4k vs 109.5k
+    GCUPS, profiles/r1/bench_k_ab.log) and on strips (113.7-114.1k vs 99.2-101.0k, strip_k_ab.log); bounded boards
+    too since round 3's staged passes (127.5k vs 119.2k GCUPS, profiles/r3/bench_bounded_job_d.log)."""
+    import ctypes
+
+    ilv, k = ctypes.c_int(), ctypes.c_int()
+    if lib.gol_default_layout(width, rows, boundary, ctypes.byref(ilv), ctypes.byref(k)) != 0:
+        raise SystemExit(f"gol_default_layout: {lib.gol_last_error().decode()}")
+    return int(ilv.value), int(k.value)
+
+
+def kernel_name(ilv: int, k: int) -> str:
+    """The dominant kernel of a pass of depth k at layout ilv (the name rocprofv3 reports, template arguments
+    aside)."""
+    if ilv == 4 and k in (16, 32):
+        return f"gol_pipe_step<D=4, S={k // 4}, P={64 // k}> (K={k}, M=4)"
+    return f"gol_stream_step<K={k}, M={ilv}>"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # VALU issue peak: 256 CUs x 4 SIMDs, each retiring one full-rate wave64 instruction per 2 cycles (32
@@ -149,6 +162,9 @@ def parse():
                    "262144); overrides --width/--height")
     p.add_argument("--tblock", type=int, default=0,
                    help="generations per pass (0 = the engine's default for the board layout)")
+    p.add_argument("--ilv", type=int, default=0, choices=(0, 1, 2, 4),
+                   help="main leg: words per interleaved block (0 = the engine's choice for the strip, gol_default_layout; "
+                   "2 with --tblock 12 = the round-5 streaming pass at 65536^2)")
     p.add_argument("--no-autotune", action="store_true",
                    help="skip the on-box race between the AUTOTUNE depths (default: race them during warmup, "
                    "interleaved, and time the faster; agreed across ranks) and use the engine default depth")
@@ -532,16 +548,18 @@ def main():
     else:
         W, H = args.width, args.height * world
     lib = _lib.load()
-    ilv = lib.gol_default_ilv(W)
+    ilv, kdef = default_layout(lib, W, args.height, boundary)  # rows per rank
+    if args.ilv:
+        ilv, kdef = args.ilv, int(lib.gol_default_tblock(args.ilv))  # (--tblock still sets the depth)
     # Temporal depth: --tblock, the engine default (--no-autotune), or by default a short on-box race between the depths
     # that are within a few percent of each other across MI355X boxes.
     if args.tblock:
         cands = [args.tblock]
     elif not args.no_autotune:
-        cands = AUTOTUNE.get(ilv, [default_depth(lib, ilv, world, args.boundary)])
+        cands = AUTOTUNE.get(ilv, [kdef])
     else:
-        cands = [default_depth(lib, ilv, world, args.boundary)]
-    runner = StripRunner(W, H, boundary, max(cands), rank=rank, world=world, device=torch.device("cuda", dev))
+        cands = [kdef]
+    runner = StripRunner(W, H, boundary, max(cands), rank=rank, world=world, device=torch.device("cuda", dev), ilv=ilv)
     runner.seed_splitmix(args.seed)
     k, tune = cands[0], None
     if len(cands) > 1:
@@ -724,7 +742,7 @@ def main():
                                    f"build's device code {fingerprint}") if traffic else
                 (f"no PMC measurement of {tkey} on this build's device code ({fingerprint})" if world == 1 else
                  "PMC traffic is measured at N = 1 only"),
-                "kernel": f"gol_stream_step<K={k}, M={ilv}>",
+                "kernel": kernel_name(ilv, k),
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": round(avg_launch_s * 1e6, 2),
             },

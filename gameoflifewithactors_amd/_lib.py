@@ -120,6 +120,7 @@ SIGNATURES = {
     "gol_default_ilv": (ctypes.c_int, [i64]),
     "gol_default_tblock": (ctypes.c_int, [ctypes.c_int]),
     "gol_supported_k": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "gol_default_layout": (ctypes.c_int, [i64, i64, ctypes.c_int, ip, ip]),
     "gol_last_error": (ctypes.c_char_p, []),
     "gol_version": (ctypes.c_char_p, []),
     "gol_arch_supported": (ctypes.c_int, [ctypes.c_char_p]),
@@ -143,6 +144,8 @@ SIGNATURES = {
     "gol_debug_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64]),
     "gol_debug_get_option": (ctypes.c_int, [vp, ctypes.c_char_p, i64p]),
     "gol_debug_option_names": (ctypes.c_char_p, []),
+    "gol_debug_pipe_plan": (ctypes.c_int, [sp, ctypes.c_int, i64, i64, i64, i64p, i64]),
+    "gol_debug_pipe_errors": (ctypes.c_int, [ip]),
 }
 
 # Names gol_debug_set_option / gol_debug_get_option take (csrc/gol_debug.h); Board.set_option routes them there.

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgol_hip.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("gol_step.hip", "gol_formats.hip", "gol_resident.hip", "gol_wave.hip", "gol_coop.hip", "gol_lanes.hip", "gol_capi.cpp", "gol_multi.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("gol_step.hip", "gol_formats.hip", "gol_resident.hip", "gol_wave.hip", "gol_coop.hip", "gol_lanes.hip", "gol_pipe.hip", "gol_capi.cpp", "gol_multi.cpp")]
 HEADERS = [
     os.path.join(CSRC, "gol_bitlogic.h"),
     os.path.join(CSRC, "gol_layout.h"),

@@ -189,9 +189,18 @@ constexpr int kCoopFlagWords = 1024;            // bands of one launch at most (
 constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
 constexpr int64_t kCoopMaxGensPerLaunch = 32768;  // a launch's granule tags count its blocks in 16 bits
 
+// The level-pipelined pass (gol_pipe.hip): torus boards (or strips) of at least this many cells whose
+// rows hold at least one full strip of 62 blocks of 128 cells get ilv 4 and its depth.
+constexpr int64_t kPipeMinCells = (int64_t)1 << 30;
+constexpr int kPipeK = 32;
+bool pipe_shape(int64_t width, int64_t rows, int boundary) {
+    return boundary == GOL_TORUS && width % 128 == 0 && width / 128 >= 62 && width * rows >= kPipeMinCells;
+}
+
 // Layout and depth a new board gets when the caller leaves them at 0.  nparts: row strips (devices) of the board.
-int board_ilv(int64_t width, int64_t height, int nparts) {
+int board_ilv(int64_t width, int64_t height, int nparts, int boundary) {
     const int64_t cells = width * height;
+    if (pipe_shape(width, height / nparts, boundary)) return 4;
     // single boards the cooperative pass takes: its interleave, so a block costs 2 funnel shifts instead of 2 per
     // word (a multi-GPU board never runs that pass: it keeps the streaming layout)
     const int m = width % 32 == 0 ? gol::coop_m(width / 32) : 0;
@@ -210,8 +219,8 @@ int board_tblock(int ilv, int64_t cells, int boundary) {
     // variant); since round 3's staged passes K = 12 leads there as on the torus: the whole 10k-generation job at
     // 65536^2 127.5k vs 119.2k GCUPS (profiles/r3/bench_bounded_job_d.log).  Ghost-row strips (multi-GPU) keep
     // K = 12: over a whole job 114k vs 100k GCUPS for K = 16 (profiles/r1/strip_k_ab.log).
-    (void)boundary;
     if (ilv == 2 && cells < kMidBoardCells) return 16;
+    if (ilv == 4 && boundary == GOL_TORUS && cells >= kPipeMinCells) return kPipeK;
     return default_tblock(ilv);
 }
 
@@ -249,6 +258,9 @@ struct BoardOptions {
                                               // cooperative one, for calls of >= 2 * coop depth: 2 = where it
                                               // measured faster (use_lanes), 1 = wherever it applies, 0 = never
     int lanes_m = 0;                          // "lanes_m": its words per lane and half-row (0 = by width, 5, 9, 17)
+    int32_t pipe_split = 0;                   // "pipe_split": level-pipelined pass (gol_pipe.hip), the oldest
+                                              // pipeline's share of a pair, 1/65536 (0 = engine, < 0 = equal shares)
+    int32_t pipe_split2 = 0;                  // "pipe_split2": its ratio after the second-oldest (0 = pipe_split)
     bool coop_launch = false;                 // "coop_launch": persistent passes by hipLaunchCooperativeKernel (1), or
                                               // hipLaunchKernel after the same residency check (0, the default:
                                               // gol_internal.h launch_persistent)
@@ -258,6 +270,7 @@ struct gol_board {
     std::mutex mu;
     BoardOptions opt;
     bool invalid = false;  // a cooperative hand-off timed out: readbacks fail until the board is overwritten
+    bool invalid_pipe = false;  // ... or a ring wait of the level-pipelined pass (gol_pipe.hip)
     int device = 0;
     hipStream_t stream = nullptr;
     int64_t W = 0, H = 0;
@@ -309,6 +322,9 @@ struct gol_board {
         a.split2_opt = opt.split2;
         a.seg_opt = opt.seg_rows;
         a.seam_opt = opt.seam;
+        a.pipe_split_opt = opt.pipe_split;
+        a.pipe_split2_opt = opt.pipe_split2;
+        a.pipe_err = coop ? reinterpret_cast<int*>(coop + kCoopErrWord) : nullptr;
         return a;
     }
 };
@@ -332,10 +348,16 @@ int check_valid(gol_board* b) {
         GOL_HIP(hipStreamSynchronize(b->stream));
         if (err) {
             b->invalid = true;
+            b->invalid_pipe = (err & 2) != 0;  // gol_pipe.hip sets bit 1, the persistent passes 1
             GOL_HIP(hipMemsetAsync(b->coop + kCoopErrWord, 0, sizeof(unsigned), b->stream));
             GOL_HIP(hipStreamSynchronize(b->stream));
         }
     }
+    if (b->invalid && b->invalid_pipe)
+        return fail(GOL_ERR_HIP, "level-pipelined pass: a ring wait between the waves of one workgroup timed out (a "
+                                 "library defect: every wave it waits on is resident); creating the board with ilv 2 "
+                                 "avoids the pass; the board is invalid until it is overwritten (set_cells, load, "
+                                 "seed, clear)");
     if (b->invalid)
         return fail(GOL_ERR_HIP, "persistent pass: a band hand-off timed out -- the pass could not get every CU at "
                                  "once (another process or stream holds the device); board option \"coop\" 0 "
@@ -537,15 +559,22 @@ bool use_coop_ragged(const gol_board* b, int64_t* pitch) {
     return true;
 }
 
+// The board's error word (b->coop[kCoopErrWord]): the persistent passes' timed-out hand-offs and the level-pipelined
+// pass's timed-out ring waits (check_valid)
+int ensure_err_word(gol_board* b) {
+    if (!b->coop) {
+        GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
+        GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
+    }
+    return GOL_OK;
+}
+
 // `gens` generations of the cooperative pass on packed rows of W cells (`pitch` words, layout `ilv`; ragged_w > 0:
 // scratch rows of a ragged board of that width), ping-ponging between bufs[*cur] and bufs[*cur ^ 1]; *cur ends on
 // the result.  One launch per kCoopMaxGensPerLaunch generations.
 int coop_steps(gol_board* b, int64_t W, int64_t pitch, int ilv, int64_t ragged_w, uint32_t* const bufs[2], int* cur,
                int64_t gens, bool lanes = false) {
-    if (!b->coop) {
-        GOL_HIP(hipMalloc(&b->coop, kCoopFlagWords * sizeof(unsigned)));
-        GOL_HIP(hipMemsetAsync(b->coop, 0, kCoopFlagWords * sizeof(unsigned), b->stream));
-    }
+    if (int rc = ensure_err_word(b)) return rc;
     int nwg = 0, B = 0, R = 0;
     const int k = lanes ? lanes_depth(b) : coop_depth(b);
     int64_t need = 0;
@@ -790,6 +819,8 @@ int step_impl(gol_board* b, int64_t gens) {
         }
         return GOL_OK;
     }
+    if (b->ilv == 4)  // the level-pipelined pass reports a timed-out ring wait in the board's error word
+        if (int rc = ensure_err_word(b)) return rc;
     while (gens > 0) {
         const int k = gol::stream_largest_k(gens, b->tblock, b->ilv);
         gol::StreamArgs a = b->stream_args(0, b->H, k);
@@ -852,6 +883,15 @@ int check_strip(const gol_strip* s) {
     return GOL_OK;
 }
 
+// k = 16 / 32 at ilv 4 is the level-pipelined pass (gol_pipe.hip): torus strips with a full strip of blocks per row
+int check_pipe_strip(const gol_strip* s, int k) {
+    if (s->ilv == 4 && gol::pipe_supported(k) &&
+        !gol::pipe_applies(s->width / 32, 4, k, s->boundary == GOL_BOUNDED, 0))
+        return fail(GOL_ERR_INVALID, "k = 16 / 32 at ilv 4 is the level-pipelined pass: torus strips at least 7936 "
+                                     "cells wide (bounded strips: k <= 8 at ilv 4)");
+    return GOL_OK;
+}
+
 // StreamArgs of a strip pass (gol_strip_step / gol_strip_plan and the multi board's launches)
 gol::StreamArgs strip_args(const gol_strip* s, int64_t out_begin, int64_t out_end, int32_t split_opt, int64_t seg_opt,
                            int32_t seam_opt, int32_t split2_opt = 0) {
@@ -882,8 +922,16 @@ int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_en
                     int32_t split_opt, int64_t seg_opt, int32_t seam_opt, int32_t split2_opt) {
     if (int rc = check_strip(s)) return rc;
     if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (int rc = check_pipe_strip(s, k)) return rc;
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt, split2_opt);
+    if (s->ilv == 4 && gol::pipe_supported(k)) {  // the level-pipelined pass: 16-wave workgroups
+        gol::PipeArgs p = gol::pipe_args(a);
+        gol::plan_pipe(p, k, s->wrap_rows != 0, p.spare_waves);
+        if (seg_rows) *seg_rows = p.grows;
+        if (waves) *waves = gol::pipe_grid(p) * 16;
+        return GOL_OK;
+    }
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     if (seg_rows) *seg_rows = a.seg;
     if (waves)
@@ -897,6 +945,7 @@ int strip_step_opts(const gol_strip* s, const uint32_t* src, uint32_t* dst, int 
     if (int rc = check_strip(s)) return rc;
     if (!src || !dst || src == dst) return fail(GOL_ERR_INVALID, "src and dst must be distinct buffers");
     if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (int rc = check_pipe_strip(s, k)) return rc;
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     if (out_begin == out_end) return GOL_OK;
     if (!s->wrap_rows) {
@@ -988,7 +1037,13 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->boundary = boundary;
         b->tblock = tblock_k;
         b->packed = (width % 32) == 0;
-        b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n)) : 0;
+        b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n, boundary)) : 0;
+        // an explicit depth the level-pipelined layout does not run (12, 24 at ilv 4): the streaming layout by width
+        if (b->packed && !ilv && tblock_k && !gol::stream_supported(tblock_k, b->ilv)) b->ilv = pick_ilv(width);
+        if (b->ilv == 4 && gol::pipe_supported(tblock_k) &&
+            !gol::pipe_applies(width / 32, 4, tblock_k, boundary == GOL_BOUNDED, 0))
+            return fail(GOL_ERR_INVALID, "tblock_k 16 / 32 at ilv 4 is the level-pipelined pass: torus boards at least "
+                                         "7936 cells wide (bounded boards: tblock_k <= 8 at ilv 4)");
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
         if (!b->packed && !tblock_k && ring_by_size(width, height)) {
             // large ragged boards stream as block rows of ring_pitch(W) words: the aligned rules for that many cells
@@ -1386,6 +1441,20 @@ int gol_default_tblock(int ilv) {
     return default_tblock(ilv);
 }
 
+int gol_default_layout(int64_t width, int64_t rows, int boundary, int* ilv, int* tblock_k) {
+    if (!ilv || !tblock_k) return fail(GOL_ERR_INVALID, "null argument");
+    if (width < 32 || width % 32 || rows < 1 || (boundary != GOL_TORUS && boundary != GOL_BOUNDED))
+        return fail(GOL_ERR_INVALID, "width must be a positive multiple of 32, rows >= 1, boundary torus or bounded");
+    if (pipe_shape(width, rows, boundary)) {
+        *ilv = 4;
+        *tblock_k = kPipeK;
+    } else {
+        *ilv = pick_ilv(width);
+        *tblock_k = default_tblock(*ilv);
+    }
+    return GOL_OK;
+}
+
 int gol_supported_k(int k, int ilv) { return gol::stream_supported(k, ilv) ? 1 : 0; }
 
 int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, double* edge_us) {
@@ -1407,6 +1476,7 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
     GOL_HIP(hipEventCreate(&e0));
     hipError_t e = hipEventCreate(&e1);
     const int k = b->tblock;
+    if (b->ilv == 4 && ensure_err_word(b) != GOL_OK) e = hipErrorOutOfMemory;
     if (e == hipSuccess) e = hipEventRecord(e0, b->stream);
     if (e == hipSuccess) {
         gol::StreamArgs a = b->stream_args(0, b->H, gol::stream_largest_k(k, k, b->ilv));
@@ -1449,6 +1519,10 @@ int gol_set_option(gol_board* b, const char* name, int64_t value) {
         o.split = (int32_t)(value < 0 ? -1 : value);
     } else if (n == "seg_rows") o.seg_rows = value < 0 ? 0 : value;
     else if (n == "seam") o.seam = value < 0 ? -1 : 0;
+    else if (n == "pipe_split" || n == "pipe_split2") {
+        if (value >= 65536) return fail(GOL_ERR_INVALID, n + " must be < 65536 (1/65536 units; 0 default, < 0 equal)");
+        (n == "pipe_split" ? o.pipe_split : o.pipe_split2) = (int32_t)(value < 0 ? -1 : value);
+    }
     else if (n == "transport") {
         // multi-part boards: 1 = peer copies (the default), 2 = RCCL (distinct devices only)
         if (!b->multi) return fail(GOL_ERR_UNSUPPORTED, "transport: a single board has no halo exchange");
@@ -1554,6 +1628,8 @@ int gol_get_option(gol_board* b, const char* name, int64_t* value) {
     else if (n == "split2") *value = o.split2;
     else if (n == "seg_rows") *value = o.seg_rows;
     else if (n == "seam") *value = o.seam;
+    else if (n == "pipe_split") *value = o.pipe_split;
+    else if (n == "pipe_split2") *value = o.pipe_split2;
     else if (n == "ragged_stream") *value = o.ragged_stream;
     else if (n == "ragged_ring") *value = o.ragged_ring;
     else if (n == "coop_poll_delay") *value = o.coop_poll_delay;
@@ -1619,11 +1695,51 @@ int gol_strip_plan_ex(const gol_strip* s, int k, int64_t out_begin, int64_t out_
     if (int rc = check_strip(s)) return rc;
     if (!plan || n < 8) return fail(GOL_ERR_INVALID, "plan needs 8 entries");
     if (!gol::stream_supported(k, s->ilv)) return fail(GOL_ERR_INVALID, "k not supported for this ilv");
+    if (s->ilv == 4 && gol::pipe_supported(k))
+        return fail(GOL_ERR_UNSUPPORTED, "k = 16 / 32 at ilv 4 is the level-pipelined pass: gol_debug_pipe_plan");
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a = strip_args(s, out_begin, out_end, 0, 0, 0);
     gol::plan_stream(a, k, s->boundary == GOL_BOUNDED, s->wrap_rows != 0);
     const int64_t v[10] = {a.nstrips, a.nsegs, a.seg, a.seam, a.rem, a.rem_p, a.rem_mid, a.rem_units, a.split, a.split2};
     for (int i = 0; i < (n < 10 ? 8 : 10); i++) plan[i] = v[i];
+    return GOL_OK;
+}
+
+// The level-pipelined pass's plan for this strip pass with `wgs` resident workgroups (0: the device's), and the
+// violations a host walk of it finds (gol_pipe.hip pipe_check_plan): plan[] = nstrips, rem, rq, rp, ngroups, grows,
+// pk_lo, pk_hi, npk, nrem, P, split1, split2, grid, violations
+int gol_debug_pipe_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t wgs, int64_t* plan,
+                        int64_t n) {
+    if (int rc = check_strip(s)) return rc;
+    if (!plan || n < 15) return fail(GOL_ERR_INVALID, "plan needs 15 entries");
+    if (s->ilv != 4 || !gol::pipe_supported(k)) return fail(GOL_ERR_INVALID, "not a level-pipelined pass (ilv 4, k 16 / 32)");
+    if (int rc = check_pipe_strip(s, k)) return rc;
+    if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
+    gol::StreamArgs a = strip_args(s, out_begin, out_end, 0, 0, 0);
+    gol::PipeArgs p{};
+    p.words = a.words;
+    p.pitch = a.pitch;
+    p.rows = a.rows;
+    p.ghost = a.ghost;
+    p.out_begin = out_begin;
+    p.out_end = out_end;
+    p.spare_waves = a.spare;
+    p.wgs_opt = wgs;
+    gol::plan_pipe(p, k, s->wrap_rows != 0, p.spare_waves);
+    const int64_t v[15] = {p.nstrips, p.rem, p.rq, p.rp, p.ngroups, p.grows, p.pk_lo, p.pk_hi, p.npk, p.nrem,
+                           p.P, p.split1, p.split2, gol::pipe_grid(p), gol::pipe_check_plan(p, k, s->wrap_rows != 0)};
+    for (int i = 0; i < 15; i++) plan[i] = v[i];
+    return GOL_OK;
+}
+
+// Reads and clears the library's own error word of the level-pipelined pass (strip passes; boards use their own)
+int gol_debug_pipe_errors(int* out) {
+    if (!out) return fail(GOL_ERR_INVALID, "null argument");
+    *out = 0;
+    int* w = gol::pipe_error_word();
+    if (!w) return fail(GOL_ERR_HIP, "no device error word");
+    GOL_HIP(hipMemcpy(out, w, sizeof(int), hipMemcpyDeviceToHost));
+    GOL_HIP(hipMemset(w, 0, sizeof(int)));
     return GOL_OK;
 }
 

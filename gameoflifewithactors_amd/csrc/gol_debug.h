@@ -29,6 +29,12 @@ int gol_debug_set_option(gol_board* b, const char* name, int64_t value);
 int gol_debug_get_option(gol_board* b, const char* name, int64_t* value);
 /* The names above, comma-separated (the library's own list: _lib.DEBUG_OPTIONS is tested against it). */
 const char* gol_debug_option_names(void);
+/* Level-pipelined pass (gol_pipe.hip): its plan for a strip pass with `wgs` resident workgroups (0: the device's) and
+ * the violations a host walk of it finds -- plan[15] = nstrips, rem, rq, rp, ngroups, grows, pk_lo, pk_hi, npk, nrem,
+ * P, split1, split2, grid, violations -- and the library's own error word of its strip passes (read and cleared). */
+int gol_debug_pipe_plan(const gol_strip* s, int k, int64_t out_begin, int64_t out_end, int64_t wgs, int64_t* plan,
+                        int64_t n);
+int gol_debug_pipe_errors(int* out);
 
 #ifdef __cplusplus
 }

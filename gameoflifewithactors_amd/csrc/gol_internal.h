@@ -39,6 +39,34 @@ struct StreamArgs {
     int32_t rag_bits;   // ragged rows (width not a multiple of 32): cells in a row's last word (1..31); 0 otherwise
     int32_t rag_origin; // filled by plan_stream: ragged torus strips start at ring position -rag_origin
     int64_t rag_w;      // bounded ragged rows: the board's width in cells (cells past it are dead); 0 otherwise
+    // Level-pipelined pass (gol_pipe.hip: torus, ilv 4, K = 16 / 32): the board options "pipe_split" / "pipe_split2"
+    // (0 = the engine's, > 0 this share (1/65536), < 0 equal shares), and where a timed-out ring wait is reported (a
+    // board's error word; null: the library's own, gol_debug_pipe_errors)
+    int32_t pipe_split_opt;
+    int32_t pipe_split2_opt;
+    int* pipe_err;
+};
+
+// Geometry of one level-pipelined pass (gol_pipe.hip), filled from StreamArgs and plan_pipe.
+struct PipeArgs {
+    int64_t words, pitch, rows, ghost, out_begin, out_end;  // as StreamArgs
+    int64_t nblocks;   // blocks of 4 words per row
+    int64_t nstrips;   // full strips of 62 stored blocks
+    int32_t rem;       // blocks past the full strips (remainder workgroups), 0..30
+    int32_t rq;        // lanes per remainder sub-strip (rem + 2)
+    int32_t rp;        // remainder sub-strips per wave
+    int32_t P;         // pipelines per workgroup
+    int64_t ngroups;   // row groups per strip (a workgroup each), of grows rows (the last may be shorter)
+    int64_t grows;
+    int64_t pk_lo, pk_hi;  // groups [pk_lo, pk_hi) share remainder workgroups rp at a time; the others have one each
+    int64_t npk;       // packed remainder workgroups
+    int64_t nrem;      // remainder workgroups in all (after nstrips x ngroups)
+    int32_t split1;    // the oldest pipeline's share of a pair (1/65536, 0 = equal shares)
+    int32_t split2;    // after the second-oldest (0 = split1)
+    int64_t spare_waves;  // waves to leave free for concurrent launches
+    int64_t spin_limit;   // polls before a ring wait gives up (0 = the default)
+    int* err;             // set non-zero by a wait that gave up
+    int64_t wgs_opt;      // planning without a device (tests): resident workgroups (0 = the device's)
 };
 
 // ---- gol_step.hip
@@ -54,6 +82,20 @@ int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_b
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s);
+// PipeArgs of a pass over StreamArgs' buffer (split options, error word, spare waves)
+PipeArgs pipe_args(const StreamArgs& a);
+
+// ---- gol_pipe.hip: the level-pipelined deep pass (torus, ilv 4, K = 16 or 32)
+bool pipe_supported(int k);
+bool pipe_applies(int64_t words, int ilv, int k, bool bounded, int rag_bits);
+int pipe_default_split(int k);
+void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves);
+int64_t pipe_grid(const PipeArgs& a);  // workgroups of a planned pass (16 waves each)
+hipError_t launch_pipe_step(const uint32_t* src, uint32_t* dst, PipeArgs a, int k, bool wrap, hipStream_t s);
+int* pipe_error_word();  // the library's own error word (strip passes), device memory
+// Walks a planned pass on the host (tests): every output (row, block) stored, every row a packed remainder sub-strip
+// reads inside the buffer without a wrap or clamp, lane offsets in 32 bits.  Returns the violations found.
+int64_t pipe_check_plan(const PipeArgs& a, int k, bool wrap);
 
 // ---- gol_formats.hip
 hipError_t launch_bytes_step(const uint8_t* src, uint8_t* dst, int64_t W, int64_t H, bool bounded, hipStream_t s);

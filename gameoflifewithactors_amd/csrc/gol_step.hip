@@ -1198,15 +1198,16 @@ void gol_stream_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ ds
     X(1, 4) X(2, 4) X(4, 4) X(6, 4) X(8, 4)
 #endif
 
+// (K, ilv 4) with K = 16 / 32 is the level-pipelined pass (gol_pipe.hip, torus boards only)
 bool stream_supported(int k, int ilv) {
 #define GOL_SUP(K_, M_) \
     if (k == K_ && ilv == M_) return true;
     GOL_FOR_EACH_KM(GOL_SUP)
 #undef GOL_SUP
-    return false;
+    return ilv == 4 && pipe_supported(k);
 }
 
-int stream_max_k(int ilv) { return ilv == 1 ? 32 : (ilv == 2 ? 16 : 8); }
+int stream_max_k(int ilv) { return ilv == 1 ? 32 : (ilv == 2 ? 16 : 32); }
 
 int stream_largest_k(int64_t n, int cap, int ilv) {
     static const int ks[] = {32, 24, 16, 12, 8, 6, 4, 2, 1};
@@ -1474,8 +1475,27 @@ static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs
     return hipGetLastError();
 }
 
+PipeArgs pipe_args(const StreamArgs& a) {
+    PipeArgs p{};
+    p.words = a.words;
+    p.pitch = a.pitch;
+    p.rows = a.rows;
+    p.ghost = a.ghost;
+    p.out_begin = a.out_begin;
+    p.out_end = a.out_end;
+    p.split1 = a.pipe_split_opt;
+    p.split2 = a.pipe_split2_opt;
+    p.spare_waves = a.spare;
+    p.err = a.pipe_err ? a.pipe_err : pipe_error_word();
+    return p;
+}
+
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s) {
+    if (a.ilv == 4 && pipe_supported(k)) {  // the level-pipelined pass: torus only (callers check; see gol_pipe.hip)
+        if (!pipe_applies(a.words, a.ilv, k, bounded, a.rag_bits)) return hipErrorInvalidValue;
+        return launch_pipe_step(src, dst, pipe_args(a), k, wrap, s);
+    }
     plan_stream(a, k, bounded, wrap);
     if (a.nsegs <= 0) return hipSuccess;
 #define GOL_LAUNCH(K_, M_) \

@@ -86,8 +86,19 @@ class HipEngine:
     def __exit__(self, *exc):
         self.close()
 
-    def ilv_for(self, width: int) -> int:
-        return int(self.lib.gol_default_ilv(width))
+    def ilv_for(self, width: int, rows: int | None = None, boundary: int = TORUS) -> int:
+        """The engine's layout for a strip of this shape (gol_default_layout: ilv 4 for the level-pipelined pass's
+        torus strips); by width alone without `rows` (gol_default_ilv)."""
+        if rows is None:
+            return int(self.lib.gol_default_ilv(width))
+        return self.layout_for(width, rows, boundary)[0]
+
+    def layout_for(self, width: int, rows: int, boundary: int) -> tuple[int, int]:
+        """(ilv, k) the engine picks for a strip of `rows` rows (gol_default_layout)."""
+        ilv, k = ctypes.c_int(), ctypes.c_int()
+        check(self.lib.gol_default_layout(width, rows, boundary, ctypes.byref(ilv), ctypes.byref(k)),
+              "gol_default_layout")
+        return int(ilv.value), int(k.value)
 
     def supports_k(self, k: int, ilv: int) -> bool:
         return bool(self.lib.gol_supported_k(k, ilv))
@@ -153,7 +164,7 @@ class StripRunner:
     """One rank's strip of a width x height board; `k` generations per pass."""
 
     def __init__(self, width: int, height: int, boundary: int, k: int, rank: int = 0, world: int = 1,
-                 device: torch.device | None = None, engine=None, group=None, exchanger=None):
+                 device: torch.device | None = None, engine=None, group=None, exchanger=None, ilv: int = 0):
         if width % 32:
             raise ValueError("row strips need width % 32 == 0 (bit-packed layout)")
         if boundary not in (TORUS, BOUNDED):
@@ -167,7 +178,11 @@ class StripRunner:
         self._own_engine = engine is None  # close() releases an engine this runner created, not a caller's
         self.engine = engine if engine is not None else HipEngine(self.device)
         single = world == 1
-        ilv = getattr(self.engine, "ilv_for", lambda w: 1)(width)
+        if not ilv:  # the engine's layout for this strip's shape (ilv 4: the level-pipelined pass, k 16 / 32) ...
+            ilv_for = getattr(self.engine, "ilv_for", None)
+            ilv = ilv_for(width, rows, boundary) if ilv_for else 1
+            if ilv_for and not getattr(self.engine, "supports_k", lambda kk, m: True)(k, ilv):
+                ilv = ilv_for(width)  # ... unless it does not run the asked depth: the streaming layout by width
         if not getattr(self.engine, "supports_k", lambda kk, m: True)(k, ilv):
             raise ValueError(f"temporal block k={k} is not supported for interleave {ilv}")
         self.geom = Geometry(width, height, y0, rows, 0 if single else k, width // 32, boundary,
@@ -389,7 +404,8 @@ class LocalBoard:
     Used to exercise the strip kernels and ghost geometry on a single GPU, and as an in-process
     multi-GPU mode."""
 
-    def __init__(self, width: int, height: int, boundary: int, k: int, nstrips: int, devices=None, engine_factory=None):
+    def __init__(self, width: int, height: int, boundary: int, k: int, nstrips: int, devices=None, engine_factory=None,
+                 ilv: int = 0):
         devices = devices or [torch.device("cuda", torch.cuda.current_device())]
         self.exchange = LocalExchange()
         self.runners = []
@@ -397,7 +413,7 @@ class LocalBoard:
             dev = devices[i % len(devices)]
             eng = engine_factory(dev) if engine_factory else None
             r = StripRunner(width, height, boundary, k, rank=i, world=nstrips, device=dev, engine=eng,
-                            exchanger=self.exchange)
+                            exchanger=self.exchange, ilv=ilv)
             self.runners.append(r)
         self.exchange.runners = self.runners
         self.width, self.height, self.k = width, height, k
@@ -422,27 +438,6 @@ class LocalBoard:
         self._sync_all()  # ghost rows landed before anyone overwrites a neighbour's source buffer
         for r, q in zip(self.runners, reqs):
             r.compute(q, k)
-
-    def timed_pass(self, k: int | None = None) -> dict:
-        """One pass exactly as step_pass, timed per phase from its start (before the halo exchange is posted): to the
-        end of the interior launch, to the edge stream's release (the ghost rows landed: the halo-exchange wait) and
-        to the end of the two edge bands (the keys of the handle leg's gol_pass_timing).  HIP events on the streams
-        of a GPU strip (synchronised after the pass, not inside it); the host clock on a CPU strip.  bench.py runs a
-        few of these after its timed region for the per-rank halo figures of an N > 1 line."""
-        marks: dict = {}
-        _mark(marks, "start", self.compute_stream)
-        self.compute(self.post_exchange(k), k, marks)
-        start = marks.pop("start")
-        if isinstance(start, float):
-            us = {n: (t - start) * 1e6 for n, t in marks.items()}
-        else:
-            torch.cuda.synchronize(self.device)
-            us = {n: start.elapsed_time(ev) * 1e3 for n, ev in marks.items()}
-        out = {"interior_us": round(us["interior"], 2)}
-        if "go" in us:
-            out["edge_wait_us"] = round(us["go"], 2)
-            out["edge_done_us"] = round(us["edge"], 2)
-        return out
 
     def step(self, generations: int) -> None:
         while generations > 0:

@@ -152,6 +152,11 @@ int gol_default_ilv(int64_t width);
 int gol_device_count(int* n);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
+/* The layout and depth the engine picks for a board or row strip of `rows` rows (gol_create uses the same rule):
+ * torus boards of >= 2^30 cells at least 7936 cells wide (width % 128 == 0) run the level-pipelined pass, ilv 4 and
+ * K = 32; others as gol_default_ilv / gol_default_tblock.  k = 16 / 32 at ilv 4 is that pass: torus
+ * only (gol_strip_step refuses a bounded strip). */
+int gol_default_layout(int64_t width, int64_t rows, int boundary, int* ilv, int* tblock_k);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller (multi-GPU
  * boards: strip 0's compute stream, which every pass joins at its end). */
 int gol_stream(gol_board* b, void** stream);

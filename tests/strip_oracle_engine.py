@@ -41,7 +41,7 @@ class OracleEngine:
         self.device = torch.device("cpu")
         self.ilv = ilv
 
-    def ilv_for(self, width):
+    def ilv_for(self, width, rows=None, boundary=0):
         return self.ilv
 
     def alloc(self, geom, stream=None):

@@ -61,7 +61,64 @@ def test_layout_choice():
     lib = _lib.load()
     assert [lib.gol_default_ilv(w) for w in (100, 32, 96, 64, 320, 128, 65536)] == [0, 1, 1, 2, 2, 2, 2]
     assert all(lib.gol_supported_k(lib.gol_default_tblock(m), m) for m in (1, 2, 4))
-    assert lib.gol_supported_k(16, 4) == 0 and lib.gol_supported_k(32, 1) == 1
+    assert lib.gol_supported_k(32, 1) == 1
+    # ilv 4: the streaming pass to K = 8, then K = 16 / 32 on the level-pipelined pass (gol_pipe.hip, torus only)
+    assert [lib.gol_supported_k(k, 4) for k in (8, 12, 16, 24, 32)] == [1, 0, 1, 0, 1]
+
+
+@pytest.mark.parametrize("w,h,boundary,want", [
+    (65536, 65536, 0, (4, 32)),   # the north-star board: the level-pipelined pass
+    (65536, 65536, 1, (2, 12)),   # bounded boards keep the streaming pass
+    (32768, 32768, 0, (4, 32)),   # 2^30 cells
+    (65536, 8192, 0, (2, 12)),    # 2^29 cells: below the pass's cut-over (a 65536^2 board as 8 strips)
+    (7936, 135400, 0, (4, 32)),   # one full strip of 62 blocks per row
+    (7808, 137600, 0, (2, 12)),   # 61 blocks: no full strip
+    (65600, 65536, 0, (2, 12)),   # width % 128 != 0
+])
+def test_default_layout(w, h, boundary, want):
+    """gol_default_layout: the layout and depth gol_create picks for a board (or row strip) of this shape."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    ilv, k = ctypes.c_int(), ctypes.c_int()
+    assert lib.gol_default_layout(w, h, boundary, ctypes.byref(ilv), ctypes.byref(k)) == 0
+    assert (ilv.value, k.value) == want
+
+
+@pytest.mark.parametrize("k", [16, 32])
+@pytest.mark.parametrize("w,rows,ghost,wrap,wgs", [
+    (65536, 65536, 0, 1, 256),    # the bench board: 8 strips + 16 remainder blocks, 3 sub-strips per wave
+    (63488, 65536, 0, 1, 256),    # 8 full strips, no remainder
+    (8192, 4100, 0, 1, 256),      # 1 strip + 2 blocks: 16 sub-strips per wave
+    (16000, 9000, 0, 1, 256),     # 2 strips + 1 block
+    (12032, 3000, 0, 1, 256),     # 94 blocks: a remainder of 32 is one more (overlapping) strip
+    (65536, 8192, 32, 0, 256),    # an 8-GPU rank's ghost-row strip
+    (65536, 65536, 32, 0, 240),   # fewer workgroups (spare waves left for the edge bands)
+    (262144, 4096, 0, 1, 256),    # config 4's width (33 strips + 2 blocks), short rows: packing capped by groups
+    (65536, 37, 0, 1, 256),       # fewer rows than groups
+])
+def test_pipe_plan_covers_the_board(k, w, rows, ghost, wrap, wgs):
+    """The level-pipelined pass's plan (gol_pipe.hip plan_pipe), walked on the host (pipe_check_plan): every output
+    (row, block) is stored, every row a packed remainder sub-strip reads lies inside the buffer without a wrap or a
+    clamp (its rows are sub-strip 0's at a fixed offset), every packed group has the same rows, lane offsets fit 32
+    bits, and the grid is one round of `wgs` workgroups where the board allows it."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    lib = _lib.load()
+    s = _lib.Strip(w, rows, 0, rows, ghost, w // 32, 0, wrap, 4, 0)
+    plan = (ctypes.c_int64 * 15)()
+    assert lib.gol_debug_pipe_plan(ctypes.byref(s), k, 0, rows, wgs, plan, 15) == 0, lib.gol_last_error()
+    nstrips, rem, rq, rp, ngroups, grows, pk_lo, pk_hi, npk, nrem, p, split1, split2, grid, bad = plan
+    assert bad == 0, list(plan)
+    assert p == (4 if k == 16 else 2)
+    if nstrips * 1 + (1 if rem else 0) <= wgs and rows >= 64:
+        assert grid <= wgs, list(plan)
+    if w == 65536 and rows == 65536 and wgs == 256:  # DESIGN.md 4.7
+        assert (nstrips, rem, rq, rp, grid) == (8, 16, 18, 3, 252), list(plan)
 
 
 def test_library_reports_version_without_gpu():

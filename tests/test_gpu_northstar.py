@@ -70,7 +70,9 @@ def test_single_board_shipped_defaults(gol, name):
     c = _case(name)
     with gol.Board(c["width"], c["height"], c["boundary"]) as b:
         info = b.info()
-        assert info["ilv"] == 2 and info["tblock_k"] == 12  # both boundaries since round 3
+        # torus: the level-pipelined pass (round 6); bounded: the streaming pass's ilv 2, K = 12
+        want = (4, 32) if c["boundary"] == 0 else (2, 12)
+        assert (info["ilv"], info["tblock_k"]) == want
         b.seed_splitmix(c["seed"])
         _walk(b, c, b.step, lambda: (b.hash(), b.population()))
         assert b.generation == c["generations"]
