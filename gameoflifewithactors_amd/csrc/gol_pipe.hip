@@ -44,6 +44,12 @@
 #include "gol_bitlogic.h"
 #include "gol_internal.h"
 
+#ifndef GOL_PIPE_AB
+#define GOL_PIPE_AB 0
+#endif
+#define GOL_PIPE_STR2(x) #x
+#define GOL_PIPE_STR(x) GOL_PIPE_STR2(x)
+
 namespace gol {
 
 namespace {
@@ -69,13 +75,70 @@ __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcWord3);
 }
+// The ring's counter and row accesses are written out: the wait-count pass cannot tell them from the first stage's
+// LDS-DMA destination, and put an s_waitcnt vmcnt(0) in front of every one -- so the last stage waited for its own row
+// stores at every trip's top (and the first for its prefetch at every hand-off).  LDS operations of one wave are
+// performed in order; each read waits for its data (lgkmcnt(0)) before the asm ends; the "memory" clobbers keep the
+// compiler's own memory accesses on their side.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 __device__ __forceinline__ int lds_load(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
 }
 __device__ __forceinline__ void lds_publish(int* p, int v) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
+}
+#ifndef GOL_PIPE_POLL_ALIGN
+#define GOL_PIPE_POLL_ALIGN 6
+#endif
+// Wait until the LDS word at `p` is >= need: poll, then s_sleep 1 between polls; returns the polls left (0: gave up).
+// One asm loop whose head is aligned (GOL_PIPE_POLL_ALIGN, log2 bytes; the padding is jumped over): the compiler's own
+// loop put the head wherever the code before it ended, and the pass's speed followed that address by 25 % with an
+// 8-byte period (s_nop padding before the trip loop: 967-972 us per 65536^2 pass at an odd number of 4-byte nops,
+// 1196-1210 at an even one, profiles/r6/pipe/r6h)
+__device__ __forceinline__ int lds_wait(const int* p, int need, int limit) {
+    int left = limit, tmp;
+    asm volatile(
+        "s_branch 2f\n"
+        ".p2align " GOL_PIPE_STR(GOL_PIPE_POLL_ALIGN) "\n"
+        "1:\n\t"
+        "s_sleep 1\n\t"
+        "s_sub_i32 %[left], %[left], 1\n\t"
+        "s_cmp_le_i32 %[left], 0\n\t"
+        "s_cbranch_scc1 3f\n"
+        "2:\n\t"
+        "ds_read_b32 %[tmp], %[addr]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_gt_i32 vcc, %[need], %[tmp]\n\t"
+        "s_cbranch_vccnz 1b\n"
+        "3:"
+        : [left] "+s"(left), [tmp] "=&v"(tmp)
+        : [addr] "v"(lds_addr(p)), [need] "s"(need)
+        : "vcc", "scc", "memory");
+    return left;
+}
+// four consecutive ring rows (one trip: 4 KB from `p`, lane-major 16 bytes per lane)
+__device__ __forceinline__ void lds_read_trip(const uint32_t* p, u32x4& r0, u32x4& r1, u32x4& r2, u32x4& r3) {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+        : "v"(lds_addr(p))
+        : "memory");
+}
+__device__ __forceinline__ void lds_write_row(uint32_t* p, const u32x4& w) {
+    asm volatile("ds_write_b128 %0, %1" : : "v"(lds_addr(p)), "v"(w) : "memory");
+}
+
+// A wave-uniform 64-bit value the compiler cannot prove uniform (float math), moved to SGPRs
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // First row (relative to a group of len rows) of the i-th oldest of n pipelines: shares fall geometrically with age,
@@ -148,11 +211,46 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         ctr[p][s][1] = 0;
     }
     __syncthreads();
+#ifdef GOL_PIPE_PAD  // A/B: shift the code after the entry by GOL_PIPE_PAD 4-byte s_nops (instruction alignment study)
+    asm volatile(".rept " GOL_PIPE_STR(GOL_PIPE_PAD) "\n\ts_nop 0\n\t.endr");
+#endif
     int64_t sx, gy;
     int cnt;
-    if (!pipe_unit(a, blockIdx.x, &sx, &gy, &cnt)) return;
     int64_t y0, L;
+#if GOL_PIPE_AB == 1
+    {
+        const int64_t grp = blockIdx.x;
+        cnt = 0;
+        if (grp < a.nstrips * a.ngroups) {
+            sx = grp % a.nstrips;
+            gy = grp / a.nstrips;
+        } else {
+            const int64_t r = grp - a.nstrips * a.ngroups;
+            if (r >= a.nrem) return;
+            sx = a.nstrips;
+            if (r == a.npk || (r == a.npk + 1 && a.ngroups > 1)) {
+                gy = r == a.npk ? 0 : a.ngroups - 1;
+                cnt = 1;
+            } else {
+                gy = 1 + r * a.rp;
+                const int64_t left = a.ngroups - 1 - gy;
+                cnt = (int)(left < a.rp ? left : a.rp);
+            }
+        }
+        const int64_t g0 = gy * a.grows;
+        if (g0 >= a.rows) return;
+        const int64_t glen = a.grows < a.rows - g0 ? a.grows : a.rows - g0;
+        y0 = g0 + pipe_cut(glen, p, P, a.split1, a.split2, K);
+        L = g0 + pipe_cut(glen, p + 1, P, a.split1, a.split2, K) - y0;
+    }
+#else
+    if (!pipe_unit(a, blockIdx.x, &sx, &gy, &cnt)) return;
     pipe_rows(a, gy, p, K, &y0, &L);
+#endif
+    // the group cut is float VALU math: without this the rows and the trip count derived from them live in VGPRs, and
+    // the trip loop became an exec-masked loop (1200 against 970 us per 65536^2 pass, profiles/r6/pipe/r6g)
+    y0 = uniform64(y0);
+    L = uniform64(L);
     if (L <= 0) return;
     const int n_in = (int)(L + 2 * K - 2 * s * D);  // level-sD rows this stage reads: y0 - K + sD + i
     const int n_out = n_in - 2 * D;                 // level-(s+1)D rows it writes: y0 - K + (s+1)D + j
@@ -209,17 +307,12 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         }
     };
     bool failed = false;
+    const int spin_limit = (int)a.spin_limit;
     auto wait_ge = [&](const int* c, int need) {
-        int64_t spins = 0;
-        while (lds_load(c) < need) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > a.spin_limit) {
-                if (lane == 0) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // vector atomic; bit 1: the pipeline
-                failed = true;
-                break;
-            }
+        if (lds_wait(c, need, spin_limit) <= 0) {
+            if (lane == 0) __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // vector atomic; bit 1: the pipeline
+            failed = true;
         }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
 
     uint32_t v[kR][kM];
@@ -242,13 +335,14 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         } else {
             lds_publish(&ctr[p][s][1], kR * t);  // trip t - 1's rows were read (and used)
             wait_ge(&ctr[p][s - 1][0], kR * t + kR < n_in ? kR * t + kR : n_in);
+            u32x4 x[kR];  // the trip's 4 rows: ring slots 4t .. 4t + 3 (mod NR = 8) are one 4 KB run
+            lds_read_trip(&ring[p][s - 1][(kR * t) % NR][lane * kM], x[0], x[1], x[2], x[3]);
 #pragma unroll
             for (int r = 0; r < kR; r++) {
-                const u32x4 x = *(const u32x4*)&ring[p][s - 1][(kR * t + r) % NR][lane * kM];
-                v[r][0] = x.x;
-                v[r][1] = x.y;
-                v[r][2] = x.z;
-                v[r][3] = x.w;
+                v[r][0] = x[r].x;
+                v[r][1] = x[r].y;
+                v[r][2] = x[r].z;
+                v[r][3] = x[r].w;
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -308,8 +402,7 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
 #pragma unroll
             for (int r = 0; r < kR; r++) {
                 const int j = j0 + r;
-                if (j >= 0 && j < n_out)
-                    *(u32x4*)&ring[p][s][j % NR][lane * kM] = u32x4{v[r][0], v[r][1], v[r][2], v[r][3]};
+                if (j >= 0 && j < n_out) lds_write_row(&ring[p][s][j % NR][lane * kM], u32x4{v[r][0], v[r][1], v[r][2], v[r][3]});
             }
             lds_publish(&ctr[p][s][0], j0 + kR < n_out ? j0 + kR : n_out);
         }

@@ -61,7 +61,9 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *               2^26, 4096 or 8192 wide): ilv 2 / 4 (that pass's words per lane) and k = 16 / 8, of
  *               which it hands off every min(k, 8) generations;
  *             packed boards of 2^25 .. 2^29 cells, width % 64 == 0: ilv 2, k = 16;
- *             packed boards from 2^29 cells, width % 64 == 0: ilv 2, k = 12 -- torus and bounded alike
+ *             torus boards from 2^30 cells per part, width % 128 == 0 and >= 7936: ilv 4, k = 32 -- the
+ *               level-pipelined pass (k = 16 / 32 at ilv 4 is that pass, torus only);
+ *             other packed boards from 2^29 cells, width % 64 == 0: ilv 2, k = 12 -- torus and bounded alike
  *               (bounded boards ran k = 16 until round 3), single board or strips;
  *             other packed widths from 2^25 cells: ilv 1, k = 32;
  *             byte boards (width % 32 != 0, ilv 0) below 3 * 2^26 cells: k = 8 below 2^25 cells, 16 below 2^27,
@@ -69,7 +71,8 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *             byte boards from 3 * 2^26 cells: the rules above for the block rows they stream as (DESIGN.md 4.1
  *               "Ragged rows": 2 * ceil((W + 128) / 64) words per ring row on a torus, 2 * ceil(W / 64) when
  *               bounded; ilv 2 k = 16 below 2^29 of those cells, k = 12 above);
- *           else one of 1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k.
+ *           else one of 1,2,4,6,8,12,16,24,32 -- the engine uses the deepest supported depth <= tblock_k (a
+ *           depth the automatic ilv 4 does not run, 12 or 24, selects ilv 2 instead).
  *           A multi-part board's halo depth (gol_part_info ghost) is the deepest supported k <= tblock_k that
  *           fits its thinnest strip.
  * The initial board is all dead. */

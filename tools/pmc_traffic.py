@@ -55,8 +55,11 @@ def main():
         wr, _ = pick(cw, f"copy_w<{w}>")
         calib[w] = {"fetch_kb": f, "write_kb": wr,
                     "read_factor": gib / (f * 1024) if f else None, "write_factor": gib / (wr * 1024) if wr else None}
-    name = f"gol_stream_step<{k}, {m}, {'true' if boundary == 'bounded' else 'false'}, "
-    name += "false" if boundary == "bounded" else "true"
+    if m == 4 and k in (16, 32) and boundary == "torus":  # the level-pipelined pass (csrc/gol_pipe.hip): D, S, P, WRAP
+        name = f"gol_pipe_step<4, {k // 4}, {64 // k}, true>"
+    else:
+        name = f"gol_stream_step<{k}, {m}, {'true' if boundary == 'bounded' else 'false'}, "
+        name += "false" if boundary == "bounded" else "true"
     bf, nf = pick(per_dispatch(os.path.join(d, "bench_fetch"), "FETCH_SIZE"), name, steps)
     bw, nw = pick(per_dispatch(os.path.join(d, "bench_write"), "WRITE_SIZE"), name, steps)
     rf, wf = calib[width]["read_factor"] if width in calib else None, calib[width]["write_factor"] if width in calib else None
