@@ -822,7 +822,7 @@ int step_impl(gol_board* b, int64_t gens) {
     if (b->ilv == 4)  // the level-pipelined pass reports a timed-out ring wait in the board's error word
         if (int rc = ensure_err_word(b)) return rc;
     while (gens > 0) {
-        const int k = gol::stream_largest_k(gens, b->tblock, b->ilv);
+        const int k = gol::stream_largest_k(gens, b->tblock, b->ilv, b->W / 32, b->boundary == GOL_BOUNDED);
         gol::StreamArgs a = b->stream_args(0, b->H, k);
         GOL_HIP(gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, k, b->boundary == GOL_BOUNDED,
                                         b->boundary == GOL_TORUS, b->stream));
@@ -1040,10 +1040,6 @@ int create_impl(int64_t width, int64_t height, int boundary, const int* devices,
         b->ilv = b->packed ? (ilv ? ilv : board_ilv(width, height, n, boundary)) : 0;
         // an explicit depth the level-pipelined layout does not run (12, 24 at ilv 4): the streaming layout by width
         if (b->packed && !ilv && tblock_k && !gol::stream_supported(tblock_k, b->ilv)) b->ilv = pick_ilv(width);
-        if (b->ilv == 4 && gol::pipe_supported(tblock_k) &&
-            !gol::pipe_applies(width / 32, 4, tblock_k, boundary == GOL_BOUNDED, 0))
-            return fail(GOL_ERR_INVALID, "tblock_k 16 / 32 at ilv 4 is the level-pipelined pass: torus boards at least "
-                                         "7936 cells wide (bounded boards: tblock_k <= 8 at ilv 4)");
         b->tblock = tblock_k ? tblock_k : board_tblock(b->ilv, width * height, boundary);
         if (!b->packed && !tblock_k && ring_by_size(width, height)) {
             // large ragged boards stream as block rows of ring_pitch(W) words: the aligned rules for that many cells
@@ -1475,13 +1471,13 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
     hipEvent_t e0 = nullptr, e1 = nullptr;
     GOL_HIP(hipEventCreate(&e0));
     hipError_t e = hipEventCreate(&e1);
-    const int k = b->tblock;
+    const int k = gol::stream_largest_k(b->tblock, b->tblock, b->ilv, b->W / 32, b->boundary == GOL_BOUNDED);
     if (b->ilv == 4 && ensure_err_word(b) != GOL_OK) e = hipErrorOutOfMemory;
     if (e == hipSuccess) e = hipEventRecord(e0, b->stream);
     if (e == hipSuccess) {
-        gol::StreamArgs a = b->stream_args(0, b->H, gol::stream_largest_k(k, k, b->ilv));
-        e = gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, gol::stream_largest_k(k, k, b->ilv),
-                                    b->boundary == GOL_BOUNDED, b->boundary == GOL_TORUS, b->stream);
+        gol::StreamArgs a = b->stream_args(0, b->H, k);
+        e = gol::launch_stream_step(b->words(b->cur), b->words(b->cur ^ 1), a, k, b->boundary == GOL_BOUNDED,
+                                    b->boundary == GOL_TORUS, b->stream);
     }
     if (e == hipSuccess) e = hipEventRecord(e1, b->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
@@ -1491,7 +1487,7 @@ int gol_pass_timing(gol_board* b, int n, double* interior_us, double* wait_us, d
     if (e1) (void)hipEventDestroy(e1);
     if (e != hipSuccess) return fail(GOL_ERR_HIP, std::string("pass timing: ") + hipGetErrorString(e));
     b->cur ^= 1;
-    b->generation += gol::stream_largest_k(k, k, b->ilv);
+    b->generation += k;
     interior_us[0] = 1e3 * ms;
     wait_us[0] = 0;
     edge_us[0] = 1e3 * ms;

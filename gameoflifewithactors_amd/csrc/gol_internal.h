@@ -72,7 +72,8 @@ struct PipeArgs {
 // ---- gol_step.hip
 bool stream_supported(int k, int ilv);
 int stream_max_k(int ilv);
-int stream_largest_k(int64_t n, int cap, int ilv);
+// the deepest supported depth <= cap and <= n for rows of `words` words (words 0: never a level-pipelined depth)
+int stream_largest_k(int64_t n, int cap, int ilv, int64_t words = 0, bool bounded = false);
 // rag_bits: cells in the last word of a ragged row (words = ceil(W / 32), ilv 1), 0 for whole-word rows
 int64_t stream_strips(int64_t words, int ilv, int k, bool bounded, int rag_bits = 0);
 int stream_pair_split(int k, int ilv, bool bounded, bool wrap, bool single);

@@ -156,7 +156,7 @@ int MultiBoard::init(int64_t width, int64_t height, int boundary, const int* dev
     int64_t min_rows = height;
     for (int r = 0; r < n; r++) min_rows = std::min(min_rows, height * (r + 1) / n - height * r / n);
     // a pass of k generations reads k ghost rows on each side, which come from ONE neighbour strip
-    max_k_ = stream_largest_k(std::min<int64_t>(tblock, min_rows), tblock, ilv);
+    max_k_ = stream_largest_k(std::min<int64_t>(tblock, min_rows), tblock, ilv, width / 32, boundary == GOL_BOUNDED);
     parts_.resize((size_t)n);
     for (int r = 0; r < n; r++) {
         Part& p = parts_[(size_t)r];
@@ -546,7 +546,7 @@ int MultiBoard::step_timed(int64_t generations, int64_t* done, double* elapsed_u
 
 int MultiBoard::step(int64_t generations, int64_t* done) {
     while (generations > 0) {
-        const int k = stream_largest_k(generations, max_k_, ilv_);
+        const int k = stream_largest_k(generations, max_k_, ilv_, W_ / 32, boundary_ == GOL_BOUNDED);
         GOL_MRC(pass(k));
         generations -= k;
         *done += k;

@@ -1209,10 +1209,14 @@ bool stream_supported(int k, int ilv) {
 
 int stream_max_k(int ilv) { return ilv == 1 ? 32 : (ilv == 2 ? 16 : 32); }
 
-int stream_largest_k(int64_t n, int cap, int ilv) {
+int stream_largest_k(int64_t n, int cap, int ilv, int64_t words, bool bounded) {
     static const int ks[] = {32, 24, 16, 12, 8, 6, 4, 2, 1};
-    for (int k : ks)
-        if (k <= cap && k <= n && stream_supported(k, ilv)) return k;
+    for (int k : ks) {
+        if (k > cap || k > n || !stream_supported(k, ilv)) continue;
+        // the level-pipelined depths (16 / 32 at ilv 4) only where that pass runs (torus rows of a full strip)
+        if (ilv == 4 && pipe_supported(k) && !pipe_applies(words, ilv, k, bounded, 0)) continue;
+        return k;
+    }
     return 1;
 }
 

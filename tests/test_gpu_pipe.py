@@ -97,13 +97,25 @@ def test_pipe_ghost_row_strips(gol, oracle):
     assert _pipe_errors() == 0
 
 
-def test_pipe_refuses_bounded_and_narrow(gol):
-    """K = 16 / 32 at ilv 4 is this pass only: a bounded board, or rows narrower than one full strip of 62 blocks,
-    are refused at creation instead of failing in a launch."""
-    with pytest.raises(ValueError, match="level-pipelined"):  # GOL_ERR_INVALID
-        gol.Board(128 * 64, 300, gol.BOUNDED, tblock_k=16, ilv=4)
-    with pytest.raises(ValueError, match="level-pipelined"):
-        gol.Board(128 * 61, 300, gol.TORUS, tblock_k=32, ilv=4)
+@pytest.mark.parametrize("w,h,boundary", [(128 * 64, 300, 1), (128 * 61, 300, 0), (512, 96, 0)])
+def test_pipe_depth_is_a_cap_where_the_pass_does_not_run(gol, oracle, w, h, boundary):
+    """tblock_k is a cap (gol.h): at ilv 4 the depths 16 / 32 are the level-pipelined pass, which runs only on torus
+    rows holding a full strip of 62 blocks; a bounded or narrower board asked for them runs the streaming pass's
+    deepest ilv-4 depth (8) instead, exact against the oracle, and a strip pass asked for them is refused."""
+    import ctypes
+
+    from gameoflifewithactors_amd import _lib
+
+    b0 = _rand(h, w, w + h + boundary)
+    gens = 37
+    with gol.Board(w, h, boundary, tblock_k=32, ilv=4, options={"coop": 0}) as b:
+        b.set_cells(b0).step(gens)
+        got = b.get_cells()
+    np.testing.assert_array_equal(got, oracle.c_run(b0, gens, boundary))
+    lib = _lib.load()
+    s = _lib.Strip(w, h, 0, h, 0, w // 32, boundary, 1 if boundary == 0 else 0, 4, 0)
+    rc = lib.gol_strip_step(ctypes.byref(s), ctypes.c_void_p(16), ctypes.c_void_p(32), 16, 0, h, None)
+    assert rc == -1 and b"level-pipelined" in lib.gol_last_error()
 
 
 def _golden(name):
