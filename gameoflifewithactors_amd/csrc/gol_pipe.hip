@@ -91,6 +91,9 @@ __device__ __forceinline__ int lds_load(const int* p) {
 __device__ __forceinline__ void lds_publish(int* p, int v) {
     asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(v) : "memory");
 }
+#ifndef GOL_PIPE_SLEEP  // s_sleep periods (64 clocks) between polls
+#define GOL_PIPE_SLEEP 1
+#endif
 #ifndef GOL_PIPE_POLL_ALIGN
 #define GOL_PIPE_POLL_ALIGN 6
 #endif
@@ -105,7 +108,7 @@ __device__ __forceinline__ int lds_wait(const int* p, int need, int limit) {
         "s_branch 2f\n"
         ".p2align " GOL_PIPE_STR(GOL_PIPE_POLL_ALIGN) "\n"
         "1:\n\t"
-        "s_sleep 1\n\t"
+        "s_sleep " GOL_PIPE_STR(GOL_PIPE_SLEEP) "\n\t"
         "s_sub_i32 %[left], %[left], 1\n\t"
         "s_cmp_le_i32 %[left], 0\n\t"
         "s_cbranch_scc1 3f\n"
@@ -481,7 +484,7 @@ bool pipe_applies(int64_t words, int ilv, int k, bool bounded, int rag_bits) {
 
 int pipe_default_split(int k) {
     // measured at 65536^2 (tools/proto): the oldest pipeline's share of a pair
-    return k == 32 ? (int)(0.65 * 65536) : (int)(0.65 * 65536);
+    return k == 32 ? (int)(0.75 * 65536) : (int)(0.60 * 65536);
 }
 
 void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves) {

@@ -3,7 +3,7 @@
 // at least 240 generations timed by HIP events), so the two can be compared on one box.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../gameoflifewithactors_amd/csrc -o lib_pipe_bench \
 //        lib_pipe_bench.hip ../../gameoflifewithactors_amd/csrc/gol_pipe.hip
-// Usage: lib_pipe_bench W H K rounds [split]
+// Usage: lib_pipe_bench W H K rounds [split [split2]]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -36,7 +36,8 @@ __global__ void seed_k(uint32_t* b, int64_t n, uint64_t seed) {
 int main(int argc, char** argv) {
     const int64_t W = argc > 1 ? atoll(argv[1]) : 65536, H = argc > 2 ? atoll(argv[2]) : 65536;
     const int K = argc > 3 ? atoi(argv[3]) : 32, rounds = argc > 4 ? atoi(argv[4]) : 2;
-    const int split = argc > 5 ? (int)(atof(argv[5]) * 65536) : 0;
+    const int split = argc > 5 ? (int)(atof(argv[5]) * 65536) : 0;  // < 0: equal shares
+    const int split2 = argc > 6 ? (int)(atof(argv[6]) * 65536) : 0;
     const int64_t words = W / 32, n = words * H;
     uint32_t *a, *b;
     int* err;
@@ -56,6 +57,7 @@ int main(int argc, char** argv) {
     pa.out_begin = 0;
     pa.out_end = H;
     pa.split1 = split;
+    pa.split2 = split2;
     pa.err = err;
     {
         gol::PipeArgs q = pa;
