@@ -353,6 +353,11 @@ template <int M, int R, int LAY, bool BOUNDED, bool FULL>
 __global__ __launch_bounds__(kThreads) void gol_band_pass(CoopArgs a) {
     constexpr bool ILV = LAY == kLayInterleaved;
     constexpr bool RAG = LAY == kLayRagged;
+#ifdef GOL_COOP_PAD  // A/B (instruction-alignment study, round 6): GOL_COOP_PAD 4-byte s_nops at the entry
+#define GOL_COOP_STR2(x) #x
+#define GOL_COOP_STR(x) GOL_COOP_STR2(x)
+    asm volatile(".rept " GOL_COOP_STR(GOL_COOP_PAD) "\n\ts_nop 0\n\t.endr");
+#endif
     extern __shared__ uint32_t xs[];  // [2 parity][kSlots][kSlotRows][M][64 lanes]; slots 0 and kSlots - 1 stay zero
     const int band = blockIdx.x;
     const int lane = threadIdx.x & 63;
