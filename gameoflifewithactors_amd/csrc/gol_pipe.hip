@@ -534,8 +534,12 @@ void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves) {
         }
     };
     int64_t ng = wgs / a.nstrips;
+    // groups of at least 2K rows: a pipeline streams its rows plus a 2K-row cone, so a short launch (a ghost-row strip's
+    // K-row edge band) in many tiny groups would be nearly all cone; it runs in fewer, taller groups on fewer CUs
+    // (leaving the rest to the interior launch it overlaps)
+    const int64_t max_ng = rows / (2 * k) > 1 ? rows / (2 * k) : 1;
+    if (ng > max_ng) ng = max_ng;
     if (ng < 1) ng = 1;
-    if (ng > rows) ng = rows;
     for (; ng > 1; ng--) {
         fill(ng);
         if (a.nstrips * a.ngroups + a.nrem <= wgs) break;
