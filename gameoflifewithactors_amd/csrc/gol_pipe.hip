@@ -203,12 +203,22 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     __shared__ int ctr[P][S][2];                                                            // [0] rows out, [1] rows in
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if defined(GOL_PIPE_MAP) && GOL_PIPE_MAP == 1  // A/B: the stages in reverse dispatch order (the last stage oldest)
+    const int p = wave / S, s = S - 1 - (wave % S + p) % S;
+#else
     const int p = wave / S, s = (wave % S + p) % S;
+#endif
     if (lane == 0) {
         ctr[p][s][0] = 0;
         ctr[p][s][1] = 0;
     }
     __syncthreads();
+#if defined(GOL_PIPE_PRIO) && GOL_PIPE_PRIO > 0  // A/B: static wave priority by stage (MI355X_MICROARCH.md "Two waves per SIMD")
+    // 1: the later half of the stages at priority 1, 2: the earlier half, 3: the last stage, 4: the later half at
+    // priority 0 (the same code size as 1: the alignment control)
+    if (GOL_PIPE_PRIO == 1 || GOL_PIPE_PRIO == 4 ? s >= S / 2 : (GOL_PIPE_PRIO == 2 ? s < S / 2 : s == S - 1))
+        __builtin_amdgcn_s_setprio(GOL_PIPE_PRIO == 4 ? 0 : 1);
+#endif
 #ifdef GOL_PIPE_PAD  // A/B: shift the code after the entry by GOL_PIPE_PAD 4-byte s_nops (instruction alignment study)
     asm volatile(".rept " GOL_PIPE_STR(GOL_PIPE_PAD) "\n\ts_nop 0\n\t.endr");
 #endif
