@@ -41,8 +41,9 @@ def main():
                 e1.record(s)
                 b.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.gens
+                h = b.hash()
             print(json.dumps({"rep": rep, "size": a.size, "boundary": a.boundary, "options": opts,
-                              "us_per_gen": round(us, 4)}), flush=True)
+                              "us_per_gen": round(us, 4), "hash_after": h}), flush=True)
 
 
 if __name__ == "__main__":
