@@ -44,9 +44,6 @@
 #include "gol_bitlogic.h"
 #include "gol_internal.h"
 
-#ifndef GOL_PIPE_AB
-#define GOL_PIPE_AB 0
-#endif
 #define GOL_PIPE_STR2(x) #x
 #define GOL_PIPE_STR(x) GOL_PIPE_STR2(x)
 
@@ -225,36 +222,8 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     int64_t sx, gy;
     int cnt;
     int64_t y0, L;
-#if GOL_PIPE_AB == 1
-    {
-        const int64_t grp = blockIdx.x;
-        cnt = 0;
-        if (grp < a.nstrips * a.ngroups) {
-            sx = grp % a.nstrips;
-            gy = grp / a.nstrips;
-        } else {
-            const int64_t r = grp - a.nstrips * a.ngroups;
-            if (r >= a.nrem) return;
-            sx = a.nstrips;
-            if (r == a.npk || (r == a.npk + 1 && a.ngroups > 1)) {
-                gy = r == a.npk ? 0 : a.ngroups - 1;
-                cnt = 1;
-            } else {
-                gy = 1 + r * a.rp;
-                const int64_t left = a.ngroups - 1 - gy;
-                cnt = (int)(left < a.rp ? left : a.rp);
-            }
-        }
-        const int64_t g0 = gy * a.grows;
-        if (g0 >= a.rows) return;
-        const int64_t glen = a.grows < a.rows - g0 ? a.grows : a.rows - g0;
-        y0 = g0 + pipe_cut(glen, p, P, a.split1, a.split2, K);
-        L = g0 + pipe_cut(glen, p + 1, P, a.split1, a.split2, K) - y0;
-    }
-#else
     if (!pipe_unit(a, blockIdx.x, &sx, &gy, &cnt)) return;
     pipe_rows(a, gy, p, K, &y0, &L);
-#endif
     // the group cut is float VALU math: without this the rows and the trip count derived from them live in VGPRs, and
     // the trip loop became an exec-masked loop (1200 against 970 us per 65536^2 pass, profiles/r6/pipe/r6g)
     y0 = uniform64(y0);
