@@ -59,6 +59,13 @@ def kernel_name(ilv: int, k: int) -> str:
         return f"gol_pipe_step<D=4, S={k // 4}, P={64 // k}> (K={k}, M=4)"
     return f"gol_stream_step<K={k}, M={ilv}>"
 
+def hot_kernel_symbol(ilv: int, k: int) -> str:
+    """The kernel whose code object keys this configuration's PMC measurements (_lib.device_code_fingerprint): the
+    level-pipelined pass (csrc/gol_pipe.hip) at ilv 4 and K = 16 / 32, the streaming pass (csrc/gol_step.hip)
+    otherwise."""
+    return "gol_pipe_step" if ilv == 4 and k in (16, 32) else "gol_stream_step"
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # VALU issue peak: 256 CUs x 4 SIMDs, each retiring one full-rate wave64 instruction per 2 cycles (32
 # lane-slots per cycle) at 2.4 GHz.
@@ -661,7 +668,7 @@ def main():
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     slots = valu_slots_per_word_gen(ilv)
     valu_tslots = slots * (cells_gpu / 32) * k / avg_launch_s / 1e12
-    fingerprint = _lib.device_code_fingerprint()
+    fingerprint = _lib.device_code_fingerprint(kernel=hot_kernel_symbol(ilv, k))
     tkey = traffic_key(W, args.height, args.boundary, k, ilv)
     tr = (load_traffic(args.traffic_json, tkey, fingerprint) or {}) if world == 1 else {}
     traffic = tr.get("bytes_per_launch")  # measured HBM bytes per launch (rocprofv3 PMC, calibrated)

@@ -277,7 +277,10 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                 lrow = lrow + 1 == a.rows ? 0 : lrow + 1;
             } else {
                 lrow++;
-                br = br < 0 ? 0 : (br < buf_rows ? br : buf_rows - 1);
+                // 32-bit scalar compares (the buffer holds < 2^31 rows, pipe_check): the 64-bit clamp became VALU compares
+                // into VCC on stage 0's DMA issue, the pipeline's pacer
+                const int b32 = (int)br, n32 = (int)buf_rows;
+                br = b32 < 0 ? 0 : (b32 < n32 ? b32 : n32 - 1);
             }
             auto* q = (__attribute__((address_space(3))) void*)&dstage[p][par][r][0];
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(src + br * a.pitch, span), q, 16, load_off, 0, 0, 0);
@@ -590,6 +593,7 @@ hipError_t launch_pipe_step(const uint32_t* src, uint32_t* dst, PipeArgs a, int 
     const int64_t grid = pipe_grid(a);
     if (grid <= 0) return hipSuccess;
     if (!a.err) return hipErrorInvalidValue;
+    if (!wrap && a.rows + 2 * a.ghost >= ((int64_t)1 << 31)) return hipErrorInvalidValue;  // 32-bit row clamp (stage 0)
     if (a.spin_limit <= 0) a.spin_limit = (int64_t)1 << 22;  // polls of >= 64 clocks: about 0.2-0.5 s
     const dim3 block(kWave * 16);
     if (k == 16) {

@@ -197,6 +197,7 @@ class StripRunner:
                 b.record_stream(self.edge_stream)  # written by the edge stream too
         self.cur = 0
         self.generation = 0
+        self.spare_cap = None  # A/B: at most this many waves held back from the interior launch for the edge bands
         self.up = (rank - 1) % world if (boundary == TORUS or rank > 0) else None
         self.down = (rank + 1) % world if (boundary == TORUS or rank < world - 1) else None
         self.exchanger = exchanger if exchanger is not None else DistExchange(group)
@@ -259,6 +260,8 @@ class StripRunner:
             # then run alongside it as soon as the ghost rows land instead of in its tail
             plan = getattr(self.engine, "plan_waves", None)
             spare = plan(self.geom, k, 0, lo) + plan(self.geom, k, hi, h) if plan else 0
+            if self.spare_cap is not None:
+                spare = min(spare, self.spare_cap)
             self.engine.step(self.geom, src, dst, k, lo, hi, s, spare_waves=spare)
             _mark(marks, "interior", s)
             with _stream_ctx(e):

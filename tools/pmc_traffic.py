@@ -73,7 +73,7 @@ def main():
         "traffic_over_algorithmic": ((read_b + write_b) / alg) if read_b and write_b else None,
         "raw_fetch_kb": bf, "raw_write_kb": bw, "dispatches_averaged": [nf, nw], "kernel": name,
         "lane_width_bytes": width, "calibration": calib,
-        "device_code": _lib.device_code_fingerprint(),
+        "device_code": _lib.device_code_fingerprint(kernel="gol_pipe_step" if m == 4 and k in (16, 32) else "gol_stream_step"),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of bench.py (fixed depth, no "
                   "CPU baseline), the last STEPS (timed) dispatches of the kernel; corrected by traffic_calib (exact 1 "
                   "GiB copies at the same lane width)",

@@ -3,7 +3,8 @@
 // at least 240 generations timed by HIP events), so the two can be compared on one box.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../gameoflifewithactors_amd/csrc -o lib_pipe_bench \
 //        lib_pipe_bench.hip ../../gameoflifewithactors_amd/csrc/gol_pipe.hip
-// Usage: lib_pipe_bench W H K rounds [split [split2]]
+// Usage: lib_pipe_bench W H K rounds [split [split2 [wrap]]]   (wrap 0: a ghost-row strip of H rows and K ghost rows
+// per side, output rows [K, H - K): the N > 1 interior launch)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -38,7 +39,9 @@ int main(int argc, char** argv) {
     const int K = argc > 3 ? atoi(argv[3]) : 32, rounds = argc > 4 ? atoi(argv[4]) : 2;
     const int split = argc > 5 ? (int)(atof(argv[5]) * 65536) : 0;  // < 0: equal shares
     const int split2 = argc > 6 ? (int)(atof(argv[6]) * 65536) : 0;
-    const int64_t words = W / 32, n = words * H;
+    const bool wrap = argc > 7 ? atoi(argv[7]) != 0 : true;
+    const int64_t ghost = wrap ? 0 : (argc > 8 ? atoll(argv[8]) : K);  // wrap 0: ghost rows per side (the kernel's K by default)
+    const int64_t words = W / 32, n = words * (H + 2 * ghost);
     uint32_t *a, *b;
     int* err;
     CHECK(hipMalloc(&a, n * 4));
@@ -54,21 +57,22 @@ int main(int argc, char** argv) {
     pa.words = words;
     pa.pitch = words;
     pa.rows = H;
-    pa.out_begin = 0;
-    pa.out_end = H;
+    pa.ghost = ghost;
+    pa.out_begin = wrap ? 0 : K;
+    pa.out_end = wrap ? H : H - K;
     pa.split1 = split;
     pa.split2 = split2;
     pa.err = err;
     {
         gol::PipeArgs q = pa;
-        gol::plan_pipe(q, K, true, 0);
+        gol::plan_pipe(q, K, wrap, 0);
         printf("plan: nstrips %lld rem %d rq %d rp %d P %d ngroups %lld grows %lld pk [%lld, %lld) npk %lld nrem %lld "
                "split %d/%d grid %lld\n", (long long)q.nstrips, q.rem, q.rq, q.rp, q.P, (long long)q.ngroups,
                (long long)q.grows, (long long)q.pk_lo, (long long)q.pk_hi, (long long)q.npk, (long long)q.nrem, q.split1,
                q.split2, (long long)gol::pipe_grid(q));
     }
     auto pass = [&]() {
-        CHECK(gol::launch_pipe_step(a, b, pa, K, true, st));
+        CHECK(gol::launch_pipe_step(a, b, pa, K, wrap, st));
         std::swap(a, b);
     };
     seed_k<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(a, n, 0x5EEDull);
