@@ -887,8 +887,8 @@ int check_strip(const gol_strip* s) {
 int check_pipe_strip(const gol_strip* s, int k) {
     if (s->ilv == 4 && gol::pipe_supported(k) &&
         !gol::pipe_applies(s->width / 32, 4, k, s->boundary == GOL_BOUNDED, 0))
-        return fail(GOL_ERR_INVALID, "k = 16 / 32 at ilv 4 is the level-pipelined pass: torus strips at least 7936 "
-                                     "cells wide (bounded strips: k <= 8 at ilv 4)");
+        return fail(GOL_ERR_INVALID, "k = 16 / 32 at ilv 4 is the level-pipelined pass: strips at least 7936 cells wide "
+                                     "(torus) or 8192 (bounded)");
     return GOL_OK;
 }
 
@@ -926,7 +926,7 @@ int strip_plan_opts(const gol_strip* s, int k, int64_t out_begin, int64_t out_en
     if (out_begin < 0 || out_end > s->rows || out_begin > out_end) return fail(GOL_ERR_INVALID, "bad output rows");
     gol::StreamArgs a = strip_args(s, out_begin, out_end, split_opt, seg_opt, seam_opt, split2_opt);
     if (s->ilv == 4 && gol::pipe_supported(k)) {  // the level-pipelined pass: 16-wave workgroups
-        gol::PipeArgs p = gol::pipe_args(a);
+        gol::PipeArgs p = gol::pipe_args(a, s->boundary == GOL_BOUNDED);
         gol::plan_pipe(p, k, s->wrap_rows != 0, p.spare_waves);
         if (seg_rows) *seg_rows = p.grows;
         if (waves) *waves = gol::pipe_grid(p) * 16;
@@ -1721,6 +1721,7 @@ int gol_debug_pipe_plan(const gol_strip* s, int k, int64_t out_begin, int64_t ou
     p.out_end = out_end;
     p.spare_waves = a.spare;
     p.wgs_opt = wgs;
+    p.bounded = s->boundary == GOL_BOUNDED;
     gol::plan_pipe(p, k, s->wrap_rows != 0, p.spare_waves);
     const int64_t v[15] = {p.nstrips, p.rem, p.rq, p.rp, p.ngroups, p.grows, p.pk_lo, p.pk_hi, p.npk, p.nrem,
                            p.P, p.split1, p.split2, gol::pipe_grid(p), gol::pipe_check_plan(p, k, s->wrap_rows != 0)};

@@ -67,6 +67,10 @@ struct PipeArgs {
     int64_t spin_limit;   // polls before a ring wait gives up (0 = the default)
     int* err;             // set non-zero by a wait that gave up
     int64_t wgs_opt;      // planning without a device (tests): resident workgroups (0 = the device's)
+    // Bounded boards (Script.fsx:6-13): strips laid out with the board's edges on a wave's outer lanes (zero-filled
+    // lane moves), and the rows [live_lo, live_hi) (owned-row coordinates) the only live ones: rows outside stay dead
+    int32_t bounded;
+    int32_t live_lo, live_hi;
 };
 
 // ---- gol_step.hip
@@ -83,10 +87,11 @@ int stream_wpb(int64_t words, int k, int ilv, bool bounded, bool wrap, int rag_b
 void plan_stream(StreamArgs& a, int k, bool bounded, bool wrap);
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s);
-// PipeArgs of a pass over StreamArgs' buffer (split options, error word, spare waves)
-PipeArgs pipe_args(const StreamArgs& a);
+// PipeArgs of a pass over StreamArgs' buffer (split options, error word, spare waves, the live rows of a bounded board)
+PipeArgs pipe_args(const StreamArgs& a, bool bounded);
 
-// ---- gol_pipe.hip: the level-pipelined deep pass (torus, ilv 4, K = 16 or 32)
+// ---- gol_pipe.hip: the level-pipelined deep pass (ilv 4, K = 16 or 32; torus and bounded rows of >= 62 / 64 blocks;
+// a.bounded selects the bounded geometry in the functions below)
 bool pipe_supported(int k);
 bool pipe_applies(int64_t words, int ilv, int k, bool bounded, int rag_bits);
 int pipe_default_split(int k);

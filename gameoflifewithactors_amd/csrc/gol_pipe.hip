@@ -32,9 +32,13 @@
 // group cut), and pipeline p's stage s is wave S p + (s + p) mod S, so every SIMD holds every stage.  The grid is one
 // round of resident workgroups.
 //
-// Variants: WRAP (single board: the rows wrap at the board's edge, GameOfLifeDriver.fs:21-25) and ghost-row strips
-// (multi-GPU: rows outside the buffer are clamped, only ever feeding rows nobody stores).  Torus only: a bounded
-// board keeps the streaming pass (its edge-fill strips need the board's edge at a wave's outer lanes).
+// Variants: WRAP (single torus board: the rows wrap at the board's edge, GameOfLifeDriver.fs:21-25), torus ghost-row
+// strips (multi-GPU: rows outside the buffer are clamped, only ever feeding rows nobody stores), and BND (bounded
+// boards and strips, Script.fsx:6-13: dead beyond the edges).  A bounded row of nblocks >= 64 blocks is covered by
+// strips of 64 lanes whose first stores 63 blocks from the board's left edge on lane 0, whose last stores 63 up to
+// the right edge on lane 63, and whose others store 62 between halo lanes; the lane moves shift in zeros at the wave's
+// ends, which is the dead column beyond each edge at no extra instruction.  Rows outside the board load as zeros (a
+// descriptor of no bytes) and the trips that reach them zero the rows they compute there, level by level.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -63,11 +67,14 @@ constexpr int kAllButDs = 0x1 | 0x2 | 0x4 | 0x8 | 0x10 | 0x20 | 0x40 | 0x400;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i - 1 (wave_ror:1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);
+// Z (bounded boards): shifts with zero fill, so a board edge on a wave's outer lane sees dead cells beyond it
+template <bool Z>
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {  // lane i <- lane i - 1 (wave_ror:1; Z: wave_shr:1, lane 0 <- 0)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, Z ? 0x138 : 0x13C, 0xf, 0xf, Z);
 }
-__device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i + 1 (wave_rol:1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);
+template <bool Z>
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i + 1 (wave_rol:1; Z: wave_shl:1, lane 63 <- 0)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, Z ? 0x130 : 0x134, 0xf, 0xf, Z);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, kRsrcWord3);
@@ -191,7 +198,7 @@ __host__ __device__ __forceinline__ void pipe_rows(const PipeArgs& a, int64_t gy
     *L = glen > 0 ? c1 - c0 : 0;
 }
 
-template <int D, int S, int P, bool WRAP>
+template <int D, int S, int P, bool WRAP, bool BND>
 __global__ __launch_bounds__(kWave * S * P) __attribute__((amdgpu_waves_per_eu(S * P / 4)))
 void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, PipeArgs a) {
     constexpr int K = D * S, NR = kNT * kR;
@@ -237,7 +244,11 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     // (lanes rq j .. rq j + rq - 1) the halo block, the rem remainder blocks and the halo block, on group gy + j
     int64_t cb, delta = 0;
     bool stores;
-    if (cnt == 0) {
+    if (BND) {  // bounded: strip sx's lanes hold blocks c .. c + 63; the board's edges sit on lane 0 / lane 63
+        const int64_t last = a.nblocks - kWave, c = sx * kInterior < last ? sx * kInterior : last;
+        cb = c + lane;
+        stores = (c == 0 || lane >= 1) && (c == last || lane <= kInterior);
+    } else if (cnt == 0) {
         const int64_t first = sx * kInterior < a.nblocks - kInterior ? sx * kInterior : a.nblocks - kInterior;
         cb = first - 1 + lane;
         stores = lane >= 1 && lane <= kInterior;
@@ -269,6 +280,8 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     } else {
         lrow = a.ghost + y0 - K;
     }
+    // bounded: the live rows [live_lo, live_hi) in buffer rows (32-bit scalars, as the clamp below)
+    [[maybe_unused]] const int live_blo = (int)a.ghost + a.live_lo, live_bhi = (int)a.ghost + a.live_hi;
     auto dma_trip = [&](int par) {
 #pragma unroll
         for (int r = 0; r < kR; r++) {
@@ -281,9 +294,12 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                 // into VCC on stage 0's DMA issue, the pipeline's pacer
                 const int b32 = (int)br, n32 = (int)buf_rows;
                 br = b32 < 0 ? 0 : (b32 < n32 ? b32 : n32 - 1);
+                if (BND && (b32 < live_blo || b32 >= live_bhi)) br = -1;  // a dead row: loads zeros
             }
             auto* q = (__attribute__((address_space(3))) void*)&dstage[p][par][r][0];
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(src + br * a.pitch, span), q, 16, load_off, 0, 0, 0);
+            const int64_t rb = BND && br < 0 ? 0 : br;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(src + rb * a.pitch, BND && br < 0 ? 0 : span), q, 16, load_off,
+                                                     0, 0, 0);
         }
     };
     bool failed = false;
@@ -328,27 +344,42 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         __builtin_amdgcn_sched_barrier(0);
         // ---- D levels (the streaming pass's level-fenced schedule, gol_step.hip StreamWave::process): even row r takes
         // the window (X = row - 2, Y = row - 1) and leaves its sums in X, odd row r + 1 takes (Y, X)
+        // bounded: this trip's rows, level by level: after level g, v[r] is row yt + r - g - 1 (owned-row coordinates),
+        // over [yt - D, yt + kR - 2] in all; a trip reaching outside the live rows zeroes the rows it computes there
+        [[maybe_unused]] const int yt = (int)(y0 - K + s * D) + kR * t;
+        [[maybe_unused]] const bool edge_trip = BND && (yt - D < a.live_lo || yt + kR - 2 >= a.live_hi);
         uint32_t right[kR];
 #pragma unroll
-        for (int r = 0; r < kR; r++) right[r] = from_right(v[r][0]);
+        for (int r = 0; r < kR; r++) right[r] = from_right<BND>(v[r][0]);
 #pragma unroll
         for (int g = 0; g < D; g++) {
 #pragma unroll
             for (int r = 0; r < kR; r += 2) {
                 uint32_t o0[kM], o1[kM], sN[kM], cN[kM];
-                row_sum_block<kM>(v[r], from_left(v[r][kM - 1]), right[r], sN, cN);
+                row_sum_block<kM>(v[r], from_left<BND>(v[r][kM - 1]), right[r], sN, cN);
 #pragma unroll
                 for (int j = 0; j < kM; j++) {
                     o0[j] = life_next(sX[g][j], cX[g][j], sY[g][j], cY[g][j], sN[j], cN[j], aY[g][j]);
                     sX[g][j] = sN[j];
                     cX[g][j] = cN[j];
                 }
-                row_sum_block<kM>(v[r + 1], from_left(v[r + 1][kM - 1]), right[r + 1], sN, cN);
+                row_sum_block<kM>(v[r + 1], from_left<BND>(v[r + 1][kM - 1]), right[r + 1], sN, cN);
 #pragma unroll
                 for (int j = 0; j < kM; j++) {
                     o1[j] = life_next(sY[g][j], cY[g][j], sX[g][j], cX[g][j], sN[j], cN[j], v[r][j]);
                     sY[g][j] = sN[j];
                     cY[g][j] = cN[j];
+                }
+                if constexpr (BND) {
+                    if (edge_trip) {  // rows outside the board stay dead (Script.fsx:6-13)
+                        const int ya = yt + r - g - 1;
+                        const bool da = ya < a.live_lo || ya >= a.live_hi, db = ya + 1 < a.live_lo || ya + 1 >= a.live_hi;
+#pragma unroll
+                        for (int j = 0; j < kM; j++) {
+                            o0[j] = da ? 0u : o0[j];
+                            o1[j] = db ? 0u : o1[j];
+                        }
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < kM; j++) {
@@ -357,8 +388,8 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                     v[r + 1][j] = o1[j];
                 }
                 if (g + 1 < D) {
-                    right[r] = from_right(o0[0]);
-                    right[r + 1] = from_right(o1[0]);
+                    right[r] = from_right<BND>(o0[0]);
+                    right[r + 1] = from_right<BND>(o1[0]);
                     __builtin_amdgcn_sched_barrier(kAllButDs);
                 }
             }
@@ -403,25 +434,28 @@ struct PipeShape<32> {
     static constexpr int D = 4, S = 8, P = 2;
 };
 
+// Variants: the single torus board (rows wrap), torus ghost-row strips, bounded boards and strips (rows never wrap)
 template <int K>
-const void* pipe_kernel(bool wrap) {
+const void* pipe_kernel(bool wrap, bool bounded) {
     using Sh = PipeShape<K>;
-    return wrap ? (const void*)&gol_pipe_step<Sh::D, Sh::S, Sh::P, true> : (const void*)&gol_pipe_step<Sh::D, Sh::S, Sh::P, false>;
+    if (wrap) return (const void*)&gol_pipe_step<Sh::D, Sh::S, Sh::P, true, false>;
+    return bounded ? (const void*)&gol_pipe_step<Sh::D, Sh::S, Sh::P, false, true>
+                   : (const void*)&gol_pipe_step<Sh::D, Sh::S, Sh::P, false, false>;
 }
-const void* pipe_kernel_for(int k, bool wrap) {
-    if (k == 16) return pipe_kernel<16>(wrap);
-    if (k == 32) return pipe_kernel<32>(wrap);
+const void* pipe_kernel_for(int k, bool wrap, bool bounded) {
+    if (k == 16) return pipe_kernel<16>(wrap, bounded);
+    if (k == 32) return pipe_kernel<32>(wrap, bounded);
     return nullptr;
 }
 int pipe_pipelines(int k) { return k == 32 ? PipeShape<32>::P : PipeShape<16>::P; }
 
 // workgroups the device holds at once (occupancy x CUs; cached per kernel), 256 without a device (host planning)
-int64_t pipe_resident_wgs(int k, bool wrap) {
-    static std::atomic<int64_t> cache[2][2];
-    const int ki = k == 32 ? 1 : 0;
-    int64_t v = cache[ki][wrap].load(std::memory_order_relaxed);
+int64_t pipe_resident_wgs(int k, bool wrap, bool bounded) {
+    static std::atomic<int64_t> cache[2][3];
+    const int ki = k == 32 ? 1 : 0, vi = wrap ? 0 : (bounded ? 2 : 1);
+    int64_t v = cache[ki][vi].load(std::memory_order_relaxed);
     if (v > 0) return v;
-    const void* fn = pipe_kernel_for(k, wrap);
+    const void* fn = pipe_kernel_for(k, wrap, bounded);
     int dev = 0, cus = 0, blocks = 0;
     if (!fn || hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -430,7 +464,7 @@ int64_t pipe_resident_wgs(int k, bool wrap) {
         return 256;
     }
     v = (int64_t)blocks * cus;
-    cache[ki][wrap].store(v, std::memory_order_relaxed);
+    cache[ki][vi].store(v, std::memory_order_relaxed);
     return v;
 }
 
@@ -455,8 +489,10 @@ int* pipe_error_word() {
     return p;
 }
 
+// torus rows of at least one strip of stored blocks (62), bounded rows of at least one wave of blocks (64: the board's
+// edges on a strip's outer lanes)
 bool pipe_applies(int64_t words, int ilv, int k, bool bounded, int rag_bits) {
-    return !bounded && !rag_bits && ilv == kM && pipe_supported(k) && words / kM >= kInterior;
+    return !rag_bits && ilv == kM && pipe_supported(k) && words / kM >= (bounded ? kWave : kInterior);
 }
 
 int pipe_default_split(int k) {
@@ -471,7 +507,13 @@ void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves) {
     a.rem = (int32_t)(a.nblocks - a.nstrips * kInterior);
     a.rq = a.rem + 2;
     a.rp = a.rem ? kWave / a.rq : 0;
-    if (a.rem && a.rp < 2) {  // a remainder wider than 30 blocks: one more strip, overlapping the last full one
+    if (a.bounded) {  // strips of 64 blocks: the first stores 63 from the board's left edge, the last 63 up to its right
+        // edge, the ones between 62 (halo lanes on both sides); no remainder workgroups
+        a.nstrips = a.nblocks <= kWave ? 1 : 1 + (a.nblocks - kWave + kInterior - 1) / kInterior;
+        a.rem = 0;
+        a.rq = 2;
+        a.rp = 0;
+    } else if (a.rem && a.rp < 2) {  // a remainder wider than 30 blocks: one more strip, overlapping the last full one
         a.nstrips++;
         a.rem = 0;
         a.rq = 2;
@@ -483,7 +525,7 @@ void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves) {
     a.ngroups = a.grows = a.npk = a.nrem = 0;
     a.pk_lo = a.pk_hi = 0;
     if (rows <= 0) return;
-    int64_t wgs = a.wgs_opt > 0 ? a.wgs_opt : pipe_resident_wgs(k, wrap);
+    int64_t wgs = a.wgs_opt > 0 ? a.wgs_opt : pipe_resident_wgs(k, wrap, a.bounded != 0);
     const int64_t spare = (spare_waves + 15) / 16;
     wgs = wgs > spare + 1 ? wgs - spare : 1;
     const int64_t pitch_bytes = a.pitch * 4;
@@ -554,7 +596,11 @@ int64_t pipe_check_plan(const PipeArgs& a, int k, bool wrap) {
             for (int lane = 0; lane < kWave; lane++) {
                 int64_t cb, delta_rows = 0;
                 bool stores;
-                if (cnt == 0) {
+                if (a.bounded) {  // as the kernel
+                    const int64_t last = a.nblocks - kWave, c = sx * kInterior < last ? sx * kInterior : last;
+                    cb = c + lane;
+                    stores = (c == 0 || lane >= 1) && (c == last || lane <= kInterior);
+                } else if (cnt == 0) {
                     const int64_t first = sx * kInterior < a.nblocks - kInterior ? sx * kInterior : a.nblocks - kInterior;
                     cb = first - 1 + lane;
                     stores = lane >= 1 && lane <= kInterior;
@@ -594,20 +640,25 @@ hipError_t launch_pipe_step(const uint32_t* src, uint32_t* dst, PipeArgs a, int 
     if (grid <= 0) return hipSuccess;
     if (!a.err) return hipErrorInvalidValue;
     if (!wrap && a.rows + 2 * a.ghost >= ((int64_t)1 << 31)) return hipErrorInvalidValue;  // 32-bit row clamp (stage 0)
+    if (a.bounded && (wrap || a.nblocks < kWave)) return hipErrorInvalidValue;
     if (a.spin_limit <= 0) a.spin_limit = (int64_t)1 << 22;  // polls of >= 64 clocks: about 0.2-0.5 s
     const dim3 block(kWave * 16);
     if (k == 16) {
         using Sh = PipeShape<16>;
         if (wrap)
-            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, true>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, true, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+        else if (a.bounded)
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false, true>), dim3((unsigned)grid), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
     } else if (k == 32) {
         using Sh = PipeShape<32>;
         if (wrap)
-            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, true>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, true, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+        else if (a.bounded)
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false, true>), dim3((unsigned)grid), block, 0, s, src, dst, a);
         else
-            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
+            hipLaunchKernelGGL((gol_pipe_step<Sh::D, Sh::S, Sh::P, false, false>), dim3((unsigned)grid), block, 0, s, src, dst, a);
     } else {
         return hipErrorInvalidValue;
     }

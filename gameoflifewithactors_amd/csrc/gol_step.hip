@@ -1479,7 +1479,7 @@ static hipError_t launch_km(const uint32_t* src, uint32_t* dst, const StreamArgs
     return hipGetLastError();
 }
 
-PipeArgs pipe_args(const StreamArgs& a) {
+PipeArgs pipe_args(const StreamArgs& a, bool bounded) {
     PipeArgs p{};
     p.words = a.words;
     p.pitch = a.pitch;
@@ -1491,14 +1491,21 @@ PipeArgs pipe_args(const StreamArgs& a) {
     p.split2 = a.pipe_split2_opt;
     p.spare_waves = a.spare;
     p.err = a.pipe_err ? a.pipe_err : pipe_error_word();
+    p.bounded = bounded ? 1 : 0;
+    if (bounded) {  // the board's rows in owned-row coordinates, clipped to the buffer (Script.fsx:6-13)
+        const int64_t lo = -a.y0 > -a.ghost ? -a.y0 : -a.ghost;
+        const int64_t hi = a.height - a.y0 < a.rows + a.ghost ? a.height - a.y0 : a.rows + a.ghost;
+        p.live_lo = (int32_t)lo;
+        p.live_hi = (int32_t)hi;
+    }
     return p;
 }
 
 hipError_t launch_stream_step(const uint32_t* src, uint32_t* dst, StreamArgs a, int k, bool bounded, bool wrap,
                               hipStream_t s) {
-    if (a.ilv == 4 && pipe_supported(k)) {  // the level-pipelined pass: torus only (callers check; see gol_pipe.hip)
+    if (a.ilv == 4 && pipe_supported(k)) {  // the level-pipelined pass (callers check where it applies; gol_pipe.hip)
         if (!pipe_applies(a.words, a.ilv, k, bounded, a.rag_bits)) return hipErrorInvalidValue;
-        return launch_pipe_step(src, dst, pipe_args(a), k, wrap, s);
+        return launch_pipe_step(src, dst, pipe_args(a, bounded), k, wrap, s);
     }
     plan_stream(a, k, bounded, wrap);
     if (a.nsegs <= 0) return hipSuccess;

@@ -99,7 +99,8 @@ def test_default_layout(w, h, boundary, want):
     (262144, 4096, 0, 1, 256),    # config 4's width (33 strips + 2 blocks), short rows: packing capped by groups
     (65536, 37, 0, 1, 256),       # fewer rows than groups
 ])
-def test_pipe_plan_covers_the_board(k, w, rows, ghost, wrap, wgs):
+@pytest.mark.parametrize("boundary", [0, 1])
+def test_pipe_plan_covers_the_board(k, w, rows, ghost, wrap, wgs, boundary):
     """The level-pipelined pass's plan (gol_pipe.hip plan_pipe), walked on the host (pipe_check_plan): every output
     (row, block) is stored, every row a packed remainder sub-strip reads lies inside the buffer without a wrap or a
     clamp (its rows are sub-strip 0's at a fixed offset), every packed group has the same rows, lane offsets fit 32
@@ -109,7 +110,11 @@ def test_pipe_plan_covers_the_board(k, w, rows, ghost, wrap, wgs):
     from gameoflifewithactors_amd import _lib
 
     lib = _lib.load()
-    s = _lib.Strip(w, rows, 0, rows, ghost, w // 32, 0, wrap, 4, 0)
+    if boundary == 1:  # bounded: rows never wrap; rows of at least 64 blocks
+        wrap = 0
+        if w < 8192:
+            pytest.skip("bounded rows need 64 blocks")
+    s = _lib.Strip(w, rows, 0, rows, ghost, w // 32, boundary, wrap, 4, 0)
     plan = (ctypes.c_int64 * 15)()
     assert lib.gol_debug_pipe_plan(ctypes.byref(s), k, 0, rows, wgs, plan, 15) == 0, lib.gol_last_error()
     nstrips, rem, rq, rp, ngroups, grows, pk_lo, pk_hi, npk, nrem, p, split1, split2, grid, bad = plan
@@ -118,7 +123,11 @@ def test_pipe_plan_covers_the_board(k, w, rows, ghost, wrap, wgs):
     if nstrips * 1 + (1 if rem else 0) <= wgs and rows >= 64:
         assert grid <= wgs, list(plan)
     if w == 65536 and rows == 65536 and wgs == 256:
-        assert (nstrips, rem, rq, rp, grid) == (8, 16, 18, 3, 252), list(plan)
+        want = (9, 0, 2, 0, 252) if boundary else (8, 16, 18, 3, 252)  # bounded: 9 strips of 64 lanes, 28 groups
+        assert (nstrips, rem, rq, rp, grid) == want, list(plan)
+    if boundary:
+        nb = w // 128
+        assert rem == 0 and nrem == 0 and nstrips == (1 if nb <= 64 else 1 + -(-(nb - 64) // 62)), list(plan)
 
 
 def test_library_reports_version_without_gpu():

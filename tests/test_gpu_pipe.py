@@ -42,9 +42,9 @@ def _rand(h, w, seed, p=0.4):
     return (np.random.default_rng(seed).random((h, w)) < p).astype(np.uint8)
 
 
-def _run(gol, b0, k, gens, opts=None):
+def _run(gol, b0, k, gens, opts=None, boundary=0):
     h, w = b0.shape
-    with gol.Board(w, h, gol.TORUS, tblock_k=k, ilv=4, options=dict(opts or {}, coop=0)) as b:
+    with gol.Board(w, h, boundary, tblock_k=k, ilv=4, options=dict(opts or {}, coop=0)) as b:
         assert b.info()["tblock_k"] == k and b.info()["ilv"] == 4
         b.set_cells(b0).step(gens)
         return b.get_cells()
@@ -67,6 +67,59 @@ def test_pipe_matches_oracle(gol, oracle, k, nblocks, h):
     gens = 2 * k + 5  # two pipelined passes, then the streaming pass at ilv 4 for the last 5
     want = oracle.c_run(b0, gens, 0)
     np.testing.assert_array_equal(_run(gol, b0, k, gens), want)
+    assert _pipe_errors() == 0
+
+
+@pytest.mark.parametrize("k", [16, 32])
+@pytest.mark.parametrize("nblocks,h", [
+    (64, 203),    # one strip: both board edges on the wave's outer lanes
+    (65, 97),     # two strips, the second overlapping the first by 62 blocks
+    (126, 300),   # two strips meeting exactly
+    (127, 129),   # three strips
+    (190, 257),   # three strips, the last overlapping
+    (200, 41),    # fewer rows than the 2K-row cone: every group reaches past both board edges
+])
+def test_pipe_bounded_matches_oracle(gol, oracle, k, nblocks, h):
+    """Bounded boards (Script.fsx:6-13: dead beyond the edges) on the pass: strips of 64 blocks with the board's
+    edges on a wave's outer lanes (zero-filled lane moves), rows outside the board loaded as zeros and kept dead at
+    every level, against the oracle."""
+    w = 128 * nblocks
+    b0 = _rand(h, w, nblocks * 7 + h + k)
+    gens = 2 * k + 5
+    np.testing.assert_array_equal(_run(gol, b0, k, gens, boundary=1), oracle.c_run(b0, gens, 1))
+    assert _pipe_errors() == 0
+
+
+def test_pipe_bounded_live_edges(gol, oracle):
+    """Cells alive on all four edges of a bounded board: births just outside the board must never happen (a glider
+    leaving through a corner, full edge rows and columns), on the pass against the oracle."""
+    w, h, k = 128 * 65, 150, 32
+    b0 = np.zeros((h, w), np.uint8)
+    b0[0, :] = 1
+    b0[-1, :] = 1
+    b0[:, 0] = 1
+    b0[:, -1] = 1
+    b0[1:4, 1:4] = [[0, 1, 0], [0, 0, 1], [1, 1, 1]]
+    b0[60:63, w - 3:w] = [[1, 1, 1], [0, 0, 1], [0, 1, 0]]
+    gens = 3 * k + 1
+    np.testing.assert_array_equal(_run(gol, b0, k, gens, boundary=1), oracle.c_run(b0, gens, 1))
+    assert _pipe_errors() == 0
+
+
+def test_pipe_bounded_ghost_row_strips(gol, oracle):
+    """The multi-GPU rank kernel on a bounded board: 3 ghost-row strips (the end strips' outer ghost rows beyond the
+    board, dead), against the oracle."""
+    import torch
+
+    from gameoflifewithactors_amd.strips import LocalBoard
+
+    w, h, k = 128 * 66, 700, 32
+    b0 = _rand(h, w, 23)
+    with LocalBoard(w, h, 1, k, 3, ilv=4) as lb:
+        assert all(r.geom.ilv == 4 and r.geom.ghost == k for r in lb.runners)
+        lb.set_cells(torch.as_tensor(b0))
+        lb.step(3 * k + 8)
+        np.testing.assert_array_equal(lb.get_cells().numpy(), oracle.c_run(b0, 3 * k + 8, 1))
     assert _pipe_errors() == 0
 
 
@@ -97,11 +150,12 @@ def test_pipe_ghost_row_strips(gol, oracle):
     assert _pipe_errors() == 0
 
 
-@pytest.mark.parametrize("w,h,boundary", [(128 * 64, 300, 1), (128 * 61, 300, 0), (512, 96, 0)])
+@pytest.mark.parametrize("w,h,boundary", [(128 * 63, 300, 1), (128 * 61, 300, 0), (512, 96, 0)])
 def test_pipe_depth_is_a_cap_where_the_pass_does_not_run(gol, oracle, w, h, boundary):
-    """tblock_k is a cap (gol.h): at ilv 4 the depths 16 / 32 are the level-pipelined pass, which runs only on torus
-    rows holding a full strip of 62 blocks; a bounded or narrower board asked for them runs the streaming pass's
-    deepest ilv-4 depth (8) instead, exact against the oracle, and a strip pass asked for them is refused."""
+    """tblock_k is a cap (gol.h): at ilv 4 the depths 16 / 32 are the level-pipelined pass, which runs on torus rows
+    holding a full strip of 62 blocks and bounded rows of at least 64; a narrower board asked for them runs the
+    streaming pass's deepest ilv-4 depth (8) instead, exact against the oracle, and a strip pass asked for them is
+    refused."""
     import ctypes
 
     from gameoflifewithactors_amd import _lib
