@@ -189,12 +189,14 @@ constexpr int kCoopFlagWords = 1024;            // bands of one launch at most (
 constexpr int kCoopErrWord = kCoopFlagWords - 1;  // ... and the error word
 constexpr int64_t kCoopMaxGensPerLaunch = 32768;  // a launch's granule tags count its blocks in 16 bits
 
-// The level-pipelined pass (gol_pipe.hip): torus boards (or strips) of at least this many cells whose
-// rows hold at least one full strip of 62 blocks of 128 cells get ilv 4 and its depth.
+// The level-pipelined pass (gol_pipe.hip): boards (or strips) of at least this many cells whose rows
+// hold at least one strip of blocks of 128 cells -- 62 stored on a torus, 64 on a bounded board -- get ilv 4 and its
+// depth (bounded 65536^2 in the driver's window: 124.0-124.7k GCUPS against 120.9-121.7k for the streaming pass's
+// ilv 2, K = 12, profiles/r6/bounded/)
 constexpr int64_t kPipeMinCells = (int64_t)1 << 30;
 constexpr int kPipeK = 32;
 bool pipe_shape(int64_t width, int64_t rows, int boundary) {
-    return boundary == GOL_TORUS && width % 128 == 0 && width / 128 >= 62 && width * rows >= kPipeMinCells;
+    return width % 128 == 0 && width / 128 >= (boundary == GOL_TORUS ? 62 : 64) && width * rows >= kPipeMinCells;
 }
 
 // Layout and depth a new board gets when the caller leaves them at 0.  nparts: row strips (devices) of the board.
@@ -220,7 +222,7 @@ int board_tblock(int ilv, int64_t cells, int boundary) {
     // 65536^2 127.5k vs 119.2k GCUPS (profiles/r3/bench_bounded_job_d.log).  Ghost-row strips (multi-GPU) keep
     // K = 12: over a whole job 114k vs 100k GCUPS for K = 16 (profiles/r1/strip_k_ab.log).
     if (ilv == 2 && cells < kMidBoardCells) return 16;
-    if (ilv == 4 && boundary == GOL_TORUS && cells >= kPipeMinCells) return kPipeK;
+    if (ilv == 4 && cells >= kPipeMinCells) return kPipeK;
     return default_tblock(ilv);
 }
 

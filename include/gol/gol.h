@@ -61,8 +61,8 @@ typedef struct gol_board gol_board; /* opaque; library-owned */
  *               2^26, 4096 or 8192 wide): ilv 2 / 4 (that pass's words per lane) and k = 16 / 8, of
  *               which it hands off every min(k, 8) generations;
  *             packed boards of 2^25 .. 2^29 cells, width % 64 == 0: ilv 2, k = 16;
- *             torus boards from 2^30 cells per part, width % 128 == 0 and >= 7936: ilv 4, k = 32 -- the
- *               level-pipelined pass (k = 16 / 32 at ilv 4 is that pass, torus only);
+ *             boards from 2^30 cells per part, width % 128 == 0 and >= 7936 (torus) or 8192 (bounded): ilv 4,
+ *               k = 32 -- the level-pipelined pass (k = 16 / 32 at ilv 4 is that pass);
  *             other packed boards from 2^29 cells, width % 64 == 0: ilv 2, k = 12 -- torus and bounded alike
  *               (bounded boards ran k = 16 until round 3), single board or strips;
  *             other packed widths from 2^25 cells: ilv 1, k = 32;
@@ -156,9 +156,9 @@ int gol_device_count(int* n);
 int gol_default_tblock(int ilv);
 int gol_supported_k(int k, int ilv);
 /* The layout and depth the engine picks for a board or row strip of `rows` rows (gol_create uses the same rule):
- * torus boards of >= 2^30 cells at least 7936 cells wide (width % 128 == 0) run the level-pipelined pass, ilv 4 and
- * K = 32; others as gol_default_ilv / gol_default_tblock.  k = 16 / 32 at ilv 4 is that pass: torus
- * only (gol_strip_step refuses a bounded strip). */
+ * boards of >= 2^30 cells at least 7936 cells wide on a torus, 8192 bounded (width % 128 == 0) run the
+ * level-pipelined pass, ilv 4 and K = 32; others as gol_default_ilv / gol_default_tblock.  k = 16 / 32
+ * at ilv 4 is that pass (gol_strip_step refuses it on narrower strips). */
 int gol_default_layout(int64_t width, int64_t rows, int boundary, int* ilv, int* tblock_k);
 /* The HIP stream the board's kernels run on (hipStream_t), for event timing by a caller (multi-GPU
  * boards: strip 0's compute stream, which every pass joins at its end). */

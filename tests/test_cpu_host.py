@@ -62,13 +62,14 @@ def test_layout_choice():
     assert [lib.gol_default_ilv(w) for w in (100, 32, 96, 64, 320, 128, 65536)] == [0, 1, 1, 2, 2, 2, 2]
     assert all(lib.gol_supported_k(lib.gol_default_tblock(m), m) for m in (1, 2, 4))
     assert lib.gol_supported_k(32, 1) == 1
-    # ilv 4: the streaming pass to K = 8, then K = 16 / 32 on the level-pipelined pass (gol_pipe.hip, torus only)
+    # ilv 4: the streaming pass to K = 8, then K = 16 / 32 on the level-pipelined pass (gol_pipe.hip)
     assert [lib.gol_supported_k(k, 4) for k in (8, 12, 16, 24, 32)] == [1, 0, 1, 0, 1]
 
 
 @pytest.mark.parametrize("w,h,boundary,want", [
     (65536, 65536, 0, (4, 32)),   # the north-star board: the level-pipelined pass
-    (65536, 65536, 1, (2, 12)),   # bounded boards keep the streaming pass
+    (65536, 65536, 1, (4, 32)),   # bounded boards too (round 6: rows of >= 64 blocks)
+    (8064, 135000, 1, (2, 12)),   # bounded, 63 blocks: the streaming pass
     (32768, 32768, 0, (4, 32)),   # 2^30 cells
     (65536, 8192, 0, (2, 12)),    # 2^29 cells: below the pass's cut-over (a 65536^2 board as 8 strips)
     (7936, 135400, 0, (4, 32)),   # one full strip of 62 blocks per row

@@ -34,7 +34,7 @@ CASES = [
     ((32768, 16384, 0), (True, 2, 12)),      # from 2^29: ilv 2, k 12 on the torus ...
     ((32768, 16384, 1), (True, 2, 12)),      # ... and bounded (k 16 until round 3)
     ((32768, 32768, 0), (True, 4, 32)),      # torus from 2^30 cells, width % 128 == 0: the level-pipelined pass
-    ((32768, 32768, 1), (True, 2, 12)),      # ... torus only: bounded keeps the streaming pass
+    ((32768, 32768, 1), (True, 4, 32)),      # ... and bounded (rows of >= 64 blocks)
     ((8224, 4096, 0), (True, 1, 32)),        # other packed widths from 2^25 cells: ilv 1, k 32
 ]
 

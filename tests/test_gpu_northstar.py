@@ -70,8 +70,8 @@ def test_single_board_shipped_defaults(gol, name):
     c = _case(name)
     with gol.Board(c["width"], c["height"], c["boundary"]) as b:
         info = b.info()
-        # torus: the level-pipelined pass (round 6); bounded: the streaming pass's ilv 2, K = 12
-        want = (4, 32) if c["boundary"] == 0 else (2, 12)
+        # the level-pipelined pass on both boundaries (round 6)
+        want = (4, 32)
         assert (info["ilv"], info["tblock_k"]) == want
         b.seed_splitmix(c["seed"])
         _walk(b, c, b.step, lambda: (b.hash(), b.population()))
@@ -79,9 +79,10 @@ def test_single_board_shipped_defaults(gol, name):
 
 
 def test_single_board_bounded_k16(gol):
-    """The bounded board at K = 16 (its default before round 3, still the depth of mid-size boards)."""
+    """The bounded board on the streaming pass at K = 16 (its default before round 3, still the depth of mid-size
+    boards; round 6 moved the default to the level-pipelined pass)."""
     c = _case("n1_65536_bounded")
-    with gol.Board(c["width"], c["height"], c["boundary"], tblock_k=16) as b:
+    with gol.Board(c["width"], c["height"], c["boundary"], tblock_k=16, ilv=2) as b:
         assert b.info()["tblock_k"] == 16
         b.seed_splitmix(c["seed"])
         _walk(b, c, b.step, lambda: (b.hash(), b.population()))
