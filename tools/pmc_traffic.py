@@ -55,8 +55,8 @@ def main():
         wr, _ = pick(cw, f"copy_w<{w}>")
         calib[w] = {"fetch_kb": f, "write_kb": wr,
                     "read_factor": gib / (f * 1024) if f else None, "write_factor": gib / (wr * 1024) if wr else None}
-    if m == 4 and k in (16, 32) and boundary == "torus":  # the level-pipelined pass (csrc/gol_pipe.hip): D, S, P, WRAP
-        name = f"gol_pipe_step<4, {k // 4}, {64 // k}, true>"
+    if m == 4 and k in (16, 32):  # the level-pipelined pass (csrc/gol_pipe.hip): D, S, P, WRAP, BND
+        name = f"gol_pipe_step<4, {k // 4}, {64 // k}, " + ("false, true>" if boundary == "bounded" else "true, false>")
     else:
         name = f"gol_stream_step<{k}, {m}, {'true' if boundary == 'bounded' else 'false'}, "
         name += "false" if boundary == "bounded" else "true"
