@@ -51,8 +51,8 @@ struct StreamArgs {
 struct PipeArgs {
     int64_t words, pitch, rows, ghost, out_begin, out_end;  // as StreamArgs
     int64_t nblocks;   // blocks of 4 words per row
-    int64_t nstrips;   // full strips of 62 stored blocks
-    int32_t rem;       // blocks past the full strips (remainder workgroups), 0..30
+    int64_t nstrips;   // full strips of 62 stored blocks (bounded: the first and last of them store 63, at the edges)
+    int32_t rem;       // blocks past the full strips (bounded: before the last one) in remainder workgroups, 0..30
     int32_t rq;        // lanes per remainder sub-strip (rem + 2)
     int32_t rp;        // remainder sub-strips per wave
     int32_t P;         // pipelines per workgroup

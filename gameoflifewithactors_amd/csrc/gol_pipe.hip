@@ -36,7 +36,8 @@
 // strips (multi-GPU: rows outside the buffer are clamped, only ever feeding rows nobody stores), and BND (bounded
 // boards and strips, Script.fsx:6-13: dead beyond the edges).  A bounded row of nblocks >= 64 blocks is covered by
 // strips of 64 lanes whose first stores 63 blocks from the board's left edge on lane 0, whose last stores 63 up to
-// the right edge on lane 63, and whose others store 62 between halo lanes; the lane moves shift in zeros at the wave's
+// the right edge on lane 63, and whose others store 62 between halo lanes, the blocks left between the last of these and
+// the right edge strip going to remainder workgroups as on the torus; the lane moves shift in zeros at the wave's
 // ends, which is the dead column beyond each edge at no extra instruction.  Rows outside the board load as zeros (a
 // descriptor of no bytes) and the trips that reach them zero the rows they compute there, level by level.
 #include <hip/hip_runtime.h>
@@ -244,17 +245,18 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     // (lanes rq j .. rq j + rq - 1) the halo block, the rem remainder blocks and the halo block, on group gy + j
     int64_t cb, delta = 0;
     bool stores;
-    if (BND) {  // bounded: strip sx's lanes hold blocks c .. c + 63; the board's edges sit on lane 0 / lane 63
-        const int64_t last = a.nblocks - kWave, c = sx * kInterior < last ? sx * kInterior : last;
+    if (BND && cnt == 0) {  // bounded: strip sx's lanes hold blocks c .. c + 63; the board's edges on lane 0 / lane 63
+        const int64_t last = a.nblocks - kWave;
+        const int64_t c = sx + 1 < a.nstrips && sx * kInterior < last ? sx * kInterior : last;
         cb = c + lane;
         stores = (c == 0 || lane >= 1) && (c == last || lane <= kInterior);
     } else if (cnt == 0) {
         const int64_t first = sx * kInterior < a.nblocks - kInterior ? sx * kInterior : a.nblocks - kInterior;
         cb = first - 1 + lane;
         stores = lane >= 1 && lane <= kInterior;
-    } else {
+    } else {  // remainder blocks: after the full strips (torus); between the last full strip and the edge strip (bounded)
         const int j = lane / a.rq, i = lane - j * a.rq;
-        cb = a.nstrips * kInterior - 1 + i;
+        cb = a.nstrips * kInterior - (BND ? kInterior - 1 : 0) - 1 + i;
         stores = j < cnt && i >= 1 && i <= a.rem;
         delta = j < cnt ? (int64_t)j * a.grows * pitch_bytes : 0;
     }
@@ -508,12 +510,16 @@ void plan_pipe(PipeArgs& a, int k, bool wrap, int64_t spare_waves) {
     a.rq = a.rem + 2;
     a.rp = a.rem ? kWave / a.rq : 0;
     if (a.bounded) {  // strips of 64 blocks: the first stores 63 from the board's left edge, the last 63 up to its right
-        // edge, the ones between 62 (halo lanes on both sides); no remainder workgroups
-        a.nstrips = a.nblocks <= kWave ? 1 : 1 + (a.nblocks - kWave + kInterior - 1) / kInterior;
-        a.rem = 0;
-        a.rq = 2;
-        a.rp = 0;
-    } else if (a.rem && a.rp < 2) {  // a remainder wider than 30 blocks: one more strip, overlapping the last full one
+        // edge, the ones between 62 (halo lanes on both sides); the rem blocks left between the last of those and the
+        // edge strip go to remainder workgroups as on the torus
+        const int64_t edge2 = 2 * kWave - 2;  // blocks the two edge strips store
+        a.nstrips = a.nblocks <= kWave ? 1 : (a.nblocks < edge2 ? 2 : 2 + (a.nblocks - edge2) / kInterior);
+        a.rem = a.nstrips < 2 ? 0 : (int32_t)(a.nblocks - edge2 - (a.nstrips - 2) * kInterior);
+        if (a.rem < 0) a.rem = 0;  // two edge strips overlapping
+        a.rq = a.rem + 2;
+        a.rp = a.rem ? kWave / a.rq : 0;
+    }
+    if (a.rem && a.rp < 2) {  // a remainder wider than 30 blocks: one more strip, overlapping the last full one
         a.nstrips++;
         a.rem = 0;
         a.rq = 2;
@@ -596,8 +602,9 @@ int64_t pipe_check_plan(const PipeArgs& a, int k, bool wrap) {
             for (int lane = 0; lane < kWave; lane++) {
                 int64_t cb, delta_rows = 0;
                 bool stores;
-                if (a.bounded) {  // as the kernel
-                    const int64_t last = a.nblocks - kWave, c = sx * kInterior < last ? sx * kInterior : last;
+                if (a.bounded && cnt == 0) {  // as the kernel
+                    const int64_t last = a.nblocks - kWave;
+                    const int64_t c = sx + 1 < a.nstrips && sx * kInterior < last ? sx * kInterior : last;
                     cb = c + lane;
                     stores = (c == 0 || lane >= 1) && (c == last || lane <= kInterior);
                 } else if (cnt == 0) {
@@ -606,7 +613,7 @@ int64_t pipe_check_plan(const PipeArgs& a, int k, bool wrap) {
                     stores = lane >= 1 && lane <= kInterior;
                 } else {
                     const int j = lane / a.rq, i = lane - j * a.rq;
-                    cb = a.nstrips * kInterior - 1 + i;
+                    cb = a.nstrips * kInterior - (a.bounded ? kInterior - 1 : 0) - 1 + i;
                     stores = j < cnt && i >= 1 && i <= a.rem;
                     delta_rows = j < cnt ? (int64_t)j * a.grows : 0;
                     if (j < cnt && (int64_t)j * a.grows * pitch_bytes + a.nblocks * 4 * kM > (((int64_t)1 << 31) - 1)) bad++;

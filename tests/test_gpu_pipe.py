@@ -73,16 +73,17 @@ def test_pipe_matches_oracle(gol, oracle, k, nblocks, h):
 @pytest.mark.parametrize("k", [16, 32])
 @pytest.mark.parametrize("nblocks,h", [
     (64, 203),    # one strip: both board edges on the wave's outer lanes
-    (65, 97),     # two strips, the second overlapping the first by 62 blocks
-    (126, 300),   # two strips meeting exactly
-    (127, 129),   # three strips
-    (190, 257),   # three strips, the last overlapping
-    (200, 41),    # fewer rows than the 2K-row cone: every group reaches past both board edges
+    (65, 97),     # two edge strips, overlapping by 62 blocks
+    (126, 300),   # two edge strips meeting exactly
+    (127, 129),   # two edge strips and 1 remainder block between them (21 sub-strips per wave)
+    (140, 257),   # 14 remainder blocks (4 sub-strips per wave, packed over row groups)
+    (157, 150),   # a remainder of 31 blocks: one more strip instead, overlapping
+    (200, 41),    # 3 strips + 12 blocks; fewer rows than the 2K-row cone: every group reaches past both board edges
 ])
 def test_pipe_bounded_matches_oracle(gol, oracle, k, nblocks, h):
     """Bounded boards (Script.fsx:6-13: dead beyond the edges) on the pass: strips of 64 blocks with the board's
-    edges on a wave's outer lanes (zero-filled lane moves), rows outside the board loaded as zeros and kept dead at
-    every level, against the oracle."""
+    edges on a wave's outer lanes (zero-filled lane moves), remainder sub-strips between the last two, rows outside the
+    board loaded as zeros and kept dead at every level, against the oracle."""
     w = 128 * nblocks
     b0 = _rand(h, w, nblocks * 7 + h + k)
     gens = 2 * k + 5

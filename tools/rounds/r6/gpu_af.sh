@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6: bounded rows with remainder sub-strips (8 strips + 14 blocks at 65536 wide, as the torus) -- pipe tests,
+# then the bounded bench against the torus, same box
+set -e
+out=gpurun_out/r6af
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_pipe.py tests/test_gpu_strips.py > $out/pytest_pipe.log 2>&1
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --boundary bounded --no-cpu-baseline --handle-parts 0 > $out/bench_bounded_$i.log 2>&1
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --handle-parts 0 > $out/bench_torus_$i.log 2>&1
+done
