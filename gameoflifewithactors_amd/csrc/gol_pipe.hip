@@ -288,6 +288,7 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
 #pragma unroll
         for (int r = 0; r < kR; r++) {
             int64_t br = lrow;
+            bool dead = false;
             if (WRAP) {
                 lrow = lrow + 1 == a.rows ? 0 : lrow + 1;
             } else {
@@ -296,12 +297,10 @@ void gol_pipe_step(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                 // into VCC on stage 0's DMA issue, the pipeline's pacer
                 const int b32 = (int)br, n32 = (int)buf_rows;
                 br = b32 < 0 ? 0 : (b32 < n32 ? b32 : n32 - 1);
-                if (BND && (b32 < live_blo || b32 >= live_bhi)) br = -1;  // a dead row: loads zeros
+                dead = BND && (b32 < live_blo || b32 >= live_bhi);  // a dead row: loads zeros
             }
             auto* q = (__attribute__((address_space(3))) void*)&dstage[p][par][r][0];
-            const int64_t rb = BND && br < 0 ? 0 : br;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(src + rb * a.pitch, BND && br < 0 ? 0 : span), q, 16, load_off,
-                                                     0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(src + br * a.pitch, dead ? 0 : span), q, 16, load_off, 0, 0, 0);
         }
     };
     bool failed = false;
